@@ -1,0 +1,284 @@
+"""Generate tests/golden/ by importing the reference (TEST INFRASTRUCTURE ONLY).
+
+Runs ONLY in the build container, where the reference snapshot is mounted at
+/root/reference.  Nothing here travels to the GPU box: the outputs are small
+data fixtures (inputs and expected outputs) committed under tests/golden/.
+
+The reference ``self_play.py`` imports ``gym``, ``gym_go`` and ``wandb``,
+none of which is installed; minimal stand-ins are written to a temporary
+directory at run time: ``gym.make`` raises, ``govars``
+holds the six plane indices, ``gogame``/``rendering`` are empty and ``wandb``
+is a no-op.  Nothing from the reference is copied; its classes are called.
+
+Fixtures:
+  net_N{5,9,19}.npz    reference MuZeroNet (self_play.py:115-128) outputs for
+                       deterministic weights (oracle/weights.py, seed 0, C=96)
+  mcts_*.npz           reference MCTS.run (self_play.py:148-237) with
+                       random.choice and the Dirichlet draw replaced by the
+                       counter streams of oracle/rng.py: true root-child
+                       visits, root value, root priors, nodes per depth
+  game_5x5_*.npz/json  a reference run_self_play_game (self_play.py:453) over
+                       oracle.goenv.GoEnv, (a) with counter-stream hooks and
+                       (b) with the reference's own seeded RNGs
+Usage:  python -m oracle.make_golden   (from the repo root)
+"""
+import json
+import os
+import random
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+REFERENCE = "/root/reference"
+
+_STUBS = {
+    "gym/__init__.py": "def make(*a, **k):\n    raise RuntimeError('gym is not installed')\n",
+    "gym_go/__init__.py": "",
+    "gym_go/govars.py": "BLACK=0\nWHITE=1\nTURN_CHNL=2\nINVD_CHNL=3\nPASS_CHNL=4\nDONE_CHNL=5\nNUM_CHNLS=6\n",
+    "gym_go/gogame.py": "",
+    "gym_go/rendering.py": "",
+    "wandb/__init__.py": "run = None\n" + "".join(
+        f"def {f}(*a, **k):\n    return None\n" for f in ("init", "log", "save", "finish")),
+}
+
+
+def import_reference():
+    stub_dir = tempfile.mkdtemp(prefix="mzgo_stubs_")
+    for rel, text in _STUBS.items():
+        path = os.path.join(stub_dir, rel)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(text)
+    sys.dont_write_bytecode = True
+    sys.path[:0] = [stub_dir, REFERENCE]
+    import self_play as sp  # noqa: E402  (the reference module)
+    return sp
+
+
+def _ref_net(sp, sd, C, A):
+    net = sp.MuZeroNet(C, A)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return net.eval()
+
+
+def random_position(size, moves, seed):
+    """A legal position reached by uniform random play on the oracle board."""
+    from oracle import gogame
+    rng = np.random.default_rng(seed)
+    st = gogame.init_state(size)
+    for _ in range(moves):
+        if gogame.game_ended(st):
+            break
+        legal = np.flatnonzero(gogame.invalid_moves(st) == 0)
+        legal = legal[legal < size * size]          # keep the game going
+        if len(legal) == 0:
+            break
+        st = gogame.next_state(st, int(rng.choice(legal)))
+    return st
+
+
+def make_net(sp, N, B, C=96, seed=0):
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    sd = deterministic_state_dict(C, A, seed)
+    net = _ref_net(sp, sd, C, A)
+    rng = np.random.default_rng(1000 + N)
+    obs = np.stack([random_position(N, int(rng.integers(0, N * N)), 7 * N + b) for b in range(B)])
+    act = rng.integers(0, A, size=B).astype(np.int64)
+    with torch.no_grad():
+        lat, v0, lg0 = net.initial_inference(torch.FloatTensor(obs))
+        nl, r1, v1, lg1 = net.recurrent_inference(lat, torch.from_numpy(act))
+        # fp64 truth of the same computation (tolerance reasoning only)
+        net64 = _ref_net(sp, sd, C, A).double()
+        lat64, v064, lg064 = net64.initial_inference(torch.from_numpy(obs))
+        nl64, r164, v164, lg164 = net64.recurrent_inference(lat.double(), torch.from_numpy(act))
+    out = dict(obs=obs.astype(np.float64), action=act, latent=lat.numpy(), value0=v0.numpy(),
+               logits0=lg0.numpy(), next_latent=nl.numpy(), reward1=r1.numpy(), value1=v1.numpy(),
+               logits1=lg1.numpy(), latent_f64=lat64.numpy(), value0_f64=v064.numpy(),
+               logits0_f64=lg064.numpy(), next_latent_f64=nl64.numpy(), reward1_f64=r164.numpy(),
+               value1_f64=v164.numpy(), logits1_f64=lg164.numpy(), seed=np.int64(seed), C=np.int64(C))
+    np.savez_compressed(os.path.join(GOLDEN, f"net_N{N}.npz"), **out)
+    print("net", N, {k: v.shape for k, v in out.items()})
+
+
+class _Hooked:
+    """Counter-stream hooks installed into the reference module."""
+
+    def __init__(self, sp, seed, game):
+        from oracle.rng import SearchHooks
+        self.sp, self.seed, self.game = sp, seed, game
+        self.move, self.sim, self.in_search = 0, -1, False
+        self.hooks = SearchHooks(seed, game, 0)
+        self.saved = (sp.random.choice, sp.np.random.choice, sp.apply_dirichlet_noise,
+                      sp.MCTS.select_leaf, sp.MCTS.run, sp.MuZeroAgent.select_action)
+
+    def install(self, eps_noise=True):
+        from oracle.rng import SearchHooks, injected_noise
+        sp, me = self.sp, self
+        orig_choice, orig_npchoice, _, orig_select, orig_run, orig_act = self.saved
+
+        def choice(seq):
+            if me.in_search:
+                return seq[me.hooks.choice_index(len(seq), me.sim)]
+            return seq[me.hooks.action_index(len(seq))]
+
+        def np_choice(a, p=None, **kw):
+            from oracle.selfplay import inverse_cdf
+            return inverse_cdf(np.asarray(p), me.hooks.action_uniform())
+
+        def noise(policy, alpha, epsilon):
+            d = injected_noise(me.seed, me.game, me.move, len(policy))
+            return (1 - epsilon) * policy + epsilon * d
+
+        def select_leaf(self_, node, valid_mask):
+            me.sim += 1
+            return orig_select(self_, node, valid_mask)
+
+        def run(self_, observation):
+            me.in_search, me.sim = True, -1
+            try:
+                return orig_run(self_, observation)
+            finally:
+                me.in_search = False
+
+        def select_action(self_, observation, temperature):
+            me.hooks = SearchHooks(me.seed, me.game, me.move)
+            try:
+                return orig_act(self_, observation, temperature)
+            finally:
+                me.move += 1
+
+        sp.random.choice = choice
+        sp.np.random.choice = np_choice
+        sp.apply_dirichlet_noise = noise
+        sp.MCTS.select_leaf = select_leaf
+        sp.MCTS.run = run
+        sp.MuZeroAgent.select_action = select_action
+        return self
+
+    def restore(self):
+        sp = self.sp
+        (sp.random.choice, sp.np.random.choice, sp.apply_dirichlet_noise,
+         sp.MCTS.select_leaf, sp.MCTS.run, sp.MuZeroAgent.select_action) = self.saved
+
+
+def _configure(sp, N, S):
+    sp.config.board_size = N
+    sp.config.max_action_size = N * N + 1
+    sp.config.mcts_simulations = S
+
+
+def make_mcts(sp, name, N, S, n_moves, seed=11, game=3, move=5, C=96):
+    from oracle.mcts import tree_summary
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    _configure(sp, N, S)
+    sd = deterministic_state_dict(C, A, 0)
+    net = _ref_net(sp, sd, C, A)
+    obs = random_position(N, n_moves, seed=500 + n_moves)
+    h = _Hooked(sp, seed, game)
+    h.move = move
+    h.install()
+    try:
+        from oracle.rng import SearchHooks
+        h.hooks = SearchHooks(seed, game, move)
+        mcts = sp.MCTS(net, A, S)
+        with torch.no_grad():
+            root, vc, rv = mcts.run(obs)
+    finally:
+        h.restore()
+    visits, depth = tree_summary(root, A)
+    priors = np.array([root.children[a]["prior"] for a in range(A)], dtype=np.float64)
+    out = dict(obs=obs, visits=visits, root_value=np.float64(rv), root_n=np.int64(root.visit_count),
+               returned_visit_counts=np.asarray(vc), root_priors=priors,
+               depth_hist=np.array(depth, dtype=np.int64), seed=np.int64(seed), game=np.int64(game),
+               move=np.int64(move), S=np.int64(S), N=np.int64(N), C=np.int64(C))
+    np.savez_compressed(os.path.join(GOLDEN, f"mcts_{name}.npz"), **out)
+    print("mcts", name, "root N", root.visit_count, "value", rv, "depth", depth)
+
+
+def _pack_record(rec):
+    types = {
+        "rewards": [type(r).__name__ for r in rec["rewards"]],
+        "returns": [type(r).__name__ for r in rec["returns"]],
+        "values": [type(v).__name__ for v in rec["values"]],
+        "actions": [type(a).__name__ for a in rec["actions"]],
+        "final_reward": type(rec["final_reward"]).__name__,
+        "observations": sorted({f"{o.dtype}{o.shape}" for o in rec["observations"]}),
+        "policies": sorted({f"{p.dtype}{p.shape}" for p in rec["policies"]}),
+        "keys": list(rec.keys()),
+    }
+    arrays = dict(
+        observations=np.stack(rec["observations"]),
+        actions=np.array(rec["actions"], dtype=np.int64),
+        policies=np.stack(rec["policies"]),
+        values=np.array(rec["values"], dtype=np.float64),
+        rewards=np.array(rec["rewards"], dtype=np.float64),
+        returns=np.array(rec["returns"], dtype=np.float64),
+        final_reward=np.float64(rec["final_reward"]),
+    )
+    return arrays, types
+
+
+def make_game(sp, name, N=5, S=25, C=96, seed=1234, game=0, hooked=True):
+    from oracle.goenv import GoEnv
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    _configure(sp, N, S)
+    sd = deterministic_state_dict(C, A, 0)
+    agent = sp.MuZeroAgent(N, C, A, S)
+    agent.net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    agent.net.eval()
+    env = GoEnv(N, komi=0, reward_method="real")
+    h = None
+    if hooked:
+        h = _Hooked(sp, seed, game).install()
+    else:
+        random.seed(seed)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+    import contextlib
+    import io
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            hist = sp.run_self_play_game(agent, env, sp.config)
+    finally:
+        if h:
+            h.restore()
+    rec = {
+        "observations": hist.observations, "actions": hist.actions, "policies": hist.policies,
+        "values": hist.values, "rewards": hist.rewards, "returns": hist.calculate_returns(),
+        "final_reward": hist.final_reward,
+    }
+    arrays, types = _pack_record(rec)
+    arrays.update(seed=np.int64(seed), game=np.int64(game), S=np.int64(S), N=np.int64(N), C=np.int64(C))
+    np.savez_compressed(os.path.join(GOLDEN, f"game_{name}.npz"), **arrays)
+    with open(os.path.join(GOLDEN, f"game_{name}.json"), "w") as f:
+        json.dump(types, f, indent=1)
+    print("game", name, "moves", len(hist), "final", hist.final_reward)
+
+
+def main():
+    os.makedirs(GOLDEN, exist_ok=True)
+    sys.path.insert(0, REPO)
+    sp = import_reference()
+    torch.set_num_threads(1)
+    make_net(sp, 5, 4)
+    make_net(sp, 9, 4)
+    make_net(sp, 19, 2)
+    make_mcts(sp, "5x5_s25_empty", 5, 25, 0)
+    make_mcts(sp, "5x5_s25_mid", 5, 25, 9)
+    make_mcts(sp, "9x9_s200_empty", 9, 200, 0)
+    make_mcts(sp, "9x9_s200_mid", 9, 200, 30)
+    make_mcts(sp, "9x9_s400_mid", 9, 400, 45)
+    make_mcts(sp, "19x19_s800_mid", 19, 800, 120)
+    make_game(sp, "5x5_s25_hooked", hooked=True)
+    make_game(sp, "5x5_s25_seeded", hooked=False)
+
+
+if __name__ == "__main__":
+    main()
