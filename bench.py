@@ -1,0 +1,190 @@
+"""Benchmark: MCTS simulations/sec + self-play moves/sec, 9x9 Go, 200 sims/move.
+
+BASELINE.json's metric on configs[1]: 256 parallel self-play games per GPU,
+200 simulations per move, the reference network (latent_dim 96) with
+deterministic random-init weights, fp32.  One *step* = one self-play move of
+every game on the GPU: one launch of the fused k_selfplay_move kernel
+(observation record, representation + root priors, 200 simulations of
+select / dynamics+prediction (MFMA) / expand / backup, action choice, board
+step).  Games restart (new epoch) every max_moves steps, so any --steps works.
+
+Multi-GPU (torchrun, one process per GPU): games are sharded by global id
+(rank * G + slot); no collective in the data path (scaling "weak").
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "muzero-go_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FLOPS_PER_SIM_9x9 = None  # filled from the geometry below
+
+
+def algorithmic_flops(N, C, S):
+    """Per-simulation and per-move (root) FLOPs of the reference network.
+
+    sim:  dynamics 3x3 conv 2*9*C*C*N^2 + three 1x1 heads 3*2*C*N^2 + embedding add C*N^2
+    root: representation 2*9*N^2*(6*64 + 64*64 + 64*C) + two 1x1 heads 2*2*C*N^2
+    (FCs and softmax are O(A) and omitted.)
+    """
+    cells = N * N
+    sim = 2 * 9 * C * C * cells + 3 * 2 * C * cells + C * cells
+    root = 2 * 9 * cells * (6 * 64 + 64 * 64 + 64 * C) + 2 * 2 * C * cells
+    return sim, root
+
+
+def cpu_baseline(N, C, S, budget_s=12.0):
+    """The oracle (CPU restatement of self_play.py's MCTS, batch-1 torch net,
+    object tree) timed on this host with one thread, on a bounded sample."""
+    import numpy as np
+
+    from oracle.mcts import MCTS
+    from oracle.net import OracleNet
+    from oracle.rng import SearchHooks, injected_noise
+    from oracle.weights import deterministic_state_dict
+    from oracle import gogame
+
+    torch.set_num_threads(1)
+    A = N * N + 1
+    net = OracleNet(deterministic_state_dict(C, A, 0))
+    st = gogame.init_state(N)
+    sims, moves, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        hooks = SearchHooks(1234, 0, moves)
+        noise = injected_noise(1234, 0, moves, A)
+        m = MCTS(net, A, S, choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+                 noise=lambda p, a, e: (1 - e) * p + e * noise)
+        with torch.no_grad():
+            m.run(st)
+        sims += S
+        legal = np.flatnonzero(gogame.invalid_moves(st) == 0)
+        st = gogame.next_state(st, int(legal[moves % len(legal)]))
+        moves += 1
+        if gogame.game_ended(st):
+            st = gogame.init_state(N)
+    dt = time.perf_counter() - t0
+    return {"value": sims / dt, "unit": "sims/s", "cores": 1, "kind": "port",
+            "sample": f"{moves} moves x {S} sims, {N}x{N}, one game, 1 thread, {dt:.1f} s "
+                      f"(oracle MCTS + torch-CPU batch-1 net; host has {os.cpu_count()} cpus)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--board-size", type=int, default=9)
+    ap.add_argument("--games", type=int, default=256, help="parallel games per GPU")
+    ap.add_argument("--sims", type=int, default=200)
+    ap.add_argument("--latent-dim", type=int, default=96)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import mzgo
+
+    N, C, S, G = args.board_size, args.latent_dim, args.sims, args.games
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).to(f"cuda:{local}").eval()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G)
+    eng = sp.engine
+    M = sp.max_moves
+    stream = torch.cuda.current_stream()
+
+    step_no = 0
+
+    def one_step():
+        nonlocal step_no
+        if step_no % M == 0:
+            sp.reset(epoch=step_no // M)
+        sp.move()
+        step_no += 1
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    c0 = eng.counters()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if step_no % M == 0:
+            sp.reset(epoch=step_no // M)
+        ev[i][0].record(stream)
+        sp.move()
+        ev[i][1].record(stream)
+        step_no += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    c1 = eng.counters()
+    sims = c1["simulations"] - c0["simulations"] if c1["simulations"] >= c0["simulations"] else c1["simulations"]
+    moves = c1["moves"] - c0["moves"] if c1["moves"] >= c0["moves"] else c1["moves"]
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    if world > 1:
+        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
+
+    if rank == 0:
+        sim_f, root_f = algorithmic_flops(N, C, S)
+        per_launch_moves = moves / world / args.steps
+        launch_flops = per_launch_moves * (S * sim_f + root_f)
+        achieved = launch_flops / avg_kern_s / 1e12
+        peak = 157.3
+        out = {
+            "metric": "MCTS simulations/sec (whole node) + self-play moves/sec, 9x9 Go, 200 sims/move",
+            "value": sims / dt,
+            "unit": "sims/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
+            "moves_per_s": moves / dt,
+            "config": {"workload": f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move",
+                       "board_size": N, "latent_dim": C, "games_per_gpu": G, "sims_per_move": S,
+                       "parallelism": f"game-sharded x{world}", "compat": "reference"},
+            "roofline": {"bound": "mfma", "kernel": "k_selfplay_move", "achieved": achieved,
+                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                         "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(N, C, S, args.cpu_budget)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,152 @@
+/* mzgo.h -- C ABI of the MI355X-native MuZero-Go self-play engine (libmzgo.so).
+ *
+ * The reference (Sir-Teo/MuZero-Go) is pure Python with no FFI; its hot path
+ * is reached through duck-typed protocols.  Each entry point below replaces
+ * one of them (citations are into the reference snapshot):
+ *
+ *   mzgo_initial_inference    MuZeroNet.initial_inference      self_play.py:121-124
+ *   mzgo_recurrent_inference  MuZeroNet.recurrent_inference    self_play.py:125-128
+ *   mzgo_set_weights          MuZeroNet.load_state_dict /       self_play.py:404-412
+ *                             MuZeroAgent.load_weights
+ *   mzgo_search               MCTS.run                         self_play.py:148-237
+ *   mzgo_board_reset          GoEnv.reset (GymGo)              self_play.py:455
+ *   mzgo_board_step           GoEnv.step  (GymGo)              self_play.py:479
+ *   mzgo_board_planes         the observation array GoEnv returns
+ *   mzgo_selfplay_move        one iteration of run_self_play_game's loop,
+ *                             for every game slot              self_play.py:465-507
+ *   mzgo_records_export       GameHistory / the pickle writer  self_play.py:415-450, :561-583
+ *
+ * Conventions
+ *   - All tensor arguments are DEVICE pointers (hipMalloc / torch CUDA tensors)
+ *     unless the name ends in _host.  Shapes are C-contiguous.
+ *   - ``stream`` is a hipStream_t (NULL = the null stream).  Calls enqueue work
+ *     and return; nothing synchronises unless documented.
+ *   - Return value: 0 on success, a negative MZGO_E* code on failure;
+ *     mzgo_last_error() then describes it (thread-local).
+ *   - An engine is not thread-safe.
+ *   - Actions are row-major cells a = r*N + c, pass = N*N (GymGo's flattening).
+ *   - Observation planes are [6][N][N]: BLACK, WHITE, TURN, INVD, PASS, DONE.
+ */
+#ifndef MZGO_H
+#define MZGO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  MZGO_OK = 0,
+  MZGO_EINVAL = -1,      /* bad argument / unsupported configuration */
+  MZGO_EHIP = -2,        /* HIP runtime error */
+  MZGO_ENOWEIGHTS = -3,  /* network weights incomplete */
+  MZGO_EASSERT = -4      /* GymGo assertion (invalid move, step after done) */
+};
+
+typedef struct mzgo_config {
+  int board_size;           /* N: 5, 6, 9 or 19 (self_play.py:20) */
+  int latent_dim;           /* C: 96 (self_play.py:21); 0 = board-only engine */
+  int num_games;            /* G: game slots held on the device */
+  int num_simulations;      /* S: MCTS simulations per move (self_play.py:23) */
+  int max_moves;            /* move cap, N*N in the reference (self_play.py:461); 0 = N*N */
+  int compat;               /* 0 = reference (zero visit counts, §0.6), 1 = fixed */
+  int temperature_moves;    /* 15 (self_play.py:29) */
+  int reserved;
+  double c_puct;            /* 2.5 (self_play.py:143) */
+  double discount;          /* 0.99 */
+  double dirichlet_alpha;   /* 0.15 */
+  double dirichlet_epsilon; /* 0.02 */
+  double pass_epsilon;      /* 0.01 */
+  double temperature;       /* 1.0 */
+  double komi;              /* 0 (self_play.py:544) */
+  uint64_t seed;            /* counter-RNG seed */
+  int game_base;            /* global id of slot 0 (multi-GPU game sharding) */
+  int device;               /* HIP device ordinal */
+} mzgo_config;
+
+typedef struct mzgo_engine mzgo_engine;
+
+/* Fill *cfg with the reference defaults (self_play.py:19-33) for board size N. */
+void mzgo_default_config(mzgo_config* cfg, int board_size);
+
+int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out);
+void mzgo_engine_destroy(mzgo_engine* eng);
+const char* mzgo_last_error(void);
+/* Bytes of device memory the engine owns. */
+int64_t mzgo_engine_device_bytes(const mzgo_engine* eng);
+
+/* Load one state_dict tensor (host float32, reference key and shape, e.g.
+ * "dynamics.conv.weight" (C,C,3,3)); packed into MFMA fragment order on upload.
+ * mzgo_weights_ready() returns 1 once all 22 keys are loaded. */
+int mzgo_set_weights(mzgo_engine* eng, const char* key, const float* data_host,
+                     const int64_t* shape, int ndim);
+int mzgo_weights_ready(const mzgo_engine* eng);
+
+/* MuZeroNet protocol, batch B (any B >= 1):
+ *   obs f32 [B][6][N][N] -> latent f32 [B][C][N][N], value f32 [B][1], logits f32 [B][N*N+1]  */
+int mzgo_initial_inference(mzgo_engine* eng, const float* obs, int B, float* latent,
+                           float* value, float* logits, void* stream);
+/*   latent f32 [B][C][N][N], action i64 [B] -> next_latent, reward [B][1], value [B][1], logits */
+int mzgo_recurrent_inference(mzgo_engine* eng, const float* latent, const int64_t* action, int B,
+                             float* next_latent, float* reward, float* value, float* logits,
+                             void* stream);
+/* Synchronises ``stream`` and reports (then clears) an out-of-range action seen
+ * by mzgo_recurrent_inference (nn.Embedding's IndexError). */
+int mzgo_check_inference_errors(mzgo_engine* eng, void* stream);
+
+/* MCTS.run for the first G slots: root_obs f32 [G][6][N][N]; noise f64 [G][A]
+ * injected Dirichlet samples or NULL (sampled from the counter RNG keyed by
+ * (seed, game_base + g, move_index)).  Outputs: root_child_visits i32 [G][A]
+ * (the true child visit counts) and root_value f64 [G] (may be NULL).  The
+ * tree stays on the device for mzgo_tree_export. */
+int mzgo_search(mzgo_engine* eng, const float* root_obs, const double* noise, int G, int move_index,
+                int32_t* root_child_visits, double* root_value, void* stream);
+/* Copy slot g's last search tree to host buffers (synchronises ``stream``):
+ * n_nodes; child i32 [n][A]; visits i32 [n]; value_sum f64 [n]; prior f32 [n][A]
+ * (row 0 unused); root_prior f64 [A].  Buffers must hold S+1 nodes; NULL skips. */
+int mzgo_tree_export(mzgo_engine* eng, int g, int32_t* n_nodes_host, int32_t* child_host,
+                     int32_t* visits_host, double* value_sum_host, float* prior_host,
+                     double* root_prior_host, void* stream);
+
+/* GoEnv protocol on the G slots.  board_step: actions i32 [G] (-1 = leave the
+ * slot alone); status i32 [G] gets 0 ok, 1 step after done, 2 invalid move,
+ * 3 action out of range; winner f64 [G] gets GoEnv.winner() after the step.
+ * status/winner may be NULL. */
+int mzgo_board_reset(mzgo_engine* eng, void* stream);
+int mzgo_board_step(mzgo_engine* eng, const int32_t* actions, int32_t* status, double* winner,
+                    void* stream);
+/* planes f64 [G][6][N][N] */
+int mzgo_board_planes(mzgo_engine* eng, double* planes, void* stream);
+/* Overwrite slot g's board (host data): stones i8 [N*N] (0/1 black/2 white),
+ * invd u8 [N*N], meta i32 [4] (turn, passed, done, moves). */
+int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uint8_t* invd_host,
+                   const int32_t* meta_host, void* stream);
+
+/* Self-play.  selfplay_reset starts a new game in every slot (epoch = RNG
+ * generation of the games); selfplay_move plays one move in every unfinished
+ * slot.  selfplay_counters (host, synchronises; cumulative over the engine's
+ * life): [0] simulations run, [1] moves played, [2] games finished, and
+ * [3] slots still playing now. */
+int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
+int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
+int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
+/* Test hook: use injected Dirichlet samples f64 [G][max_moves][A] (device,
+ * caller-owned, must outlive the moves) instead of the counter-RNG sampler;
+ * NULL restores sampling. */
+int mzgo_selfplay_inject_noise(mzgo_engine* eng, const double* noise);
+
+/* Copy slot g's game record to host buffers (synchronises ``stream``).
+ * length: moves recorded; ended: 1 if the game ended by double pass; status.
+ * stones i8 [M][N*N], invd u8 [M][N*N], flags u8 [M] (bit0 turn, bit1 passed,
+ * bit2 done), action i32 [M], value f64 [M], policy f64 [M][A], reward f64 [M],
+ * final_reward f64.  M = length; NULL pointers are skipped. */
+int mzgo_records_export(mzgo_engine* eng, int g, int32_t* length_host, int32_t* status_host,
+                        int8_t* stones_host, uint8_t* invd_host, uint8_t* flags_host,
+                        int32_t* action_host, double* value_host, double* policy_host,
+                        double* reward_host, double* final_reward_host, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MZGO_H */

@@ -1,0 +1,466 @@
+// mzgo_capi.hip -- the C ABI of include/mzgo.h: engine lifetime, device
+// memory, weight packing and dispatch to the per-(N, C) kernel tables.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mzgo.h"
+#include "mzgo_dispatch.hpp"
+
+namespace mzgo {
+extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96;
+
+const KernelSet* find_kernels(int N, int C) {
+  static const KernelSet* all[] = {&kernels_n5_c96, &kernels_n6_c96, &kernels_n9_c96, &kernels_n19_c96};
+  for (const KernelSet* k : all)
+    if (k->N == N && k->C == C) return k;
+  return nullptr;
+}
+}  // namespace mzgo
+
+using namespace mzgo;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) return fail(MZGO_EHIP, "%s: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+namespace {
+
+// Reference state_dict keys (self_play.py:63-128) and their shapes.
+struct Spec {
+  const char* key;
+  std::vector<int64_t> shape;
+};
+
+std::vector<Spec> specs(int C, int A) {
+  return {
+      {"representation.conv1.weight", {64, 6, 3, 3}}, {"representation.conv1.bias", {64}},
+      {"representation.conv2.weight", {64, 64, 3, 3}}, {"representation.conv2.bias", {64}},
+      {"representation.conv3.weight", {C, 64, 3, 3}}, {"representation.conv3.bias", {C}},
+      {"dynamics.action_embedding.weight", {A, C}},
+      {"dynamics.conv.weight", {C, C, 3, 3}}, {"dynamics.conv.bias", {C}},
+      {"dynamics.reward_conv.weight", {1, C, 1, 1}}, {"dynamics.reward_conv.bias", {1}},
+      {"dynamics.fc_reward_hidden.weight", {16, 1}}, {"dynamics.fc_reward_hidden.bias", {16}},
+      {"dynamics.fc_reward_output.weight", {1, 16}}, {"dynamics.fc_reward_output.bias", {1}},
+      {"prediction.pass_logit", {1}},
+      {"prediction.value_conv.weight", {1, C, 1, 1}}, {"prediction.value_conv.bias", {1}},
+      {"prediction.value_fc.weight", {1, 1}}, {"prediction.value_fc.bias", {1}},
+      {"prediction.policy_conv.weight", {1, C, 1, 1}}, {"prediction.policy_conv.bias", {1}},
+  };
+}
+
+// conv weight W[cout][cin][3][3] -> MFMA A-fragment order of mzgo_conv.hpp:
+// packed[((s * NCOG + cog) * 64 + lane) * MGP + mi] with k-step s = tap*CQ + c4,
+// cout = (cog*MG + mi)*16 + (lane & 15), cin = c4*4 + (lane >> 4).
+std::vector<float> pack_conv(const float* W, int COUT, int CIN) {
+  const int CINP = (CIN + 3) / 4 * 4, CQ = CINP / 4, KS = 9 * CQ;
+  const int MT = COUT / 16;
+  const int MG = (MT % 3 == 0) ? 3 : ((MT % 4 == 0 && MT >= 8) ? 4 : 2);
+  const int MGP = MG == 3 ? 4 : MG, NCOG = MT / MG;
+  std::vector<float> out((size_t)KS * NCOG * 64 * MGP, 0.f);
+  for (int s = 0; s < KS; ++s) {
+    const int t = s / CQ, c4 = s % CQ, ky = t / 3, kx = t % 3;
+    for (int cog = 0; cog < NCOG; ++cog)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int mi = 0; mi < MG; ++mi) {
+          const int cout = (cog * MG + mi) * 16 + (lane & 15);
+          const int cin = c4 * 4 + (lane >> 4);
+          const float v = cin < CIN ? W[(((size_t)cout * CIN + cin) * 3 + ky) * 3 + kx] : 0.f;
+          out[(((size_t)s * NCOG + cog) * 64 + lane) * MGP + mi] = v;
+        }
+  }
+  return out;
+}
+
+}  // namespace
+
+struct mzgo_engine {
+  mzgo_config cfg;
+  const KernelSet* ks = nullptr;
+  int N = 0, C = 0, A = 0, CELLS = 0, CS = 0, G = 0, S = 0, M = 0;
+  std::map<std::string, std::vector<float>> sd;  // host copies of the state_dict
+  std::vector<Spec> spec;
+  bool dirty = true;
+  float* d_w = nullptr;
+  size_t d_w_bytes = 0;
+  NetParams np{};
+  EngineArrays E{};
+  int* d_err = nullptr;
+  std::vector<void*> allocs;
+  int64_t bytes = 0;
+  int epoch = 0;
+  const double* noise = nullptr;
+
+  template <class T>
+  int alloc(T** p, size_t n) {
+    void* v = nullptr;
+    hipError_t e = hipMalloc(&v, n * sizeof(T) + 256);
+    if (e != hipSuccess) return fail(MZGO_EHIP, "hipMalloc(%zu): %s", n * sizeof(T), hipGetErrorString(e));
+    allocs.push_back(v);
+    bytes += (int64_t)(n * sizeof(T));
+    *p = reinterpret_cast<T*>(v);
+    return MZGO_OK;
+  }
+  ~mzgo_engine() {
+    for (void* p : allocs) (void)hipFree(p);
+    if (d_w) (void)hipFree(d_w);
+  }
+
+  // pack + upload the network if any tensor changed since the last upload
+  int sync_weights() {
+    if (C == 0) return fail(MZGO_EINVAL, "board-only engine (latent_dim 0) has no network");
+    if (!dirty) return MZGO_OK;
+    for (const Spec& s : spec)
+      if (!sd.count(s.key)) return fail(MZGO_ENOWEIGHTS, "missing weight '%s'", s.key);
+    std::vector<std::vector<float>> parts;
+    parts.push_back(pack_conv(sd["representation.conv1.weight"].data(), 64, 6));
+    parts.push_back(sd["representation.conv1.bias"]);
+    parts.push_back(pack_conv(sd["representation.conv2.weight"].data(), 64, 64));
+    parts.push_back(sd["representation.conv2.bias"]);
+    parts.push_back(pack_conv(sd["representation.conv3.weight"].data(), C, 64));
+    parts.push_back(sd["representation.conv3.bias"]);
+    parts.push_back(pack_conv(sd["dynamics.conv.weight"].data(), C, C));
+    parts.push_back(sd["dynamics.conv.bias"]);
+    parts.push_back(sd["dynamics.action_embedding.weight"]);
+    std::vector<float> hw;
+    for (const char* k : {"dynamics.reward_conv.weight", "prediction.value_conv.weight",
+                          "prediction.policy_conv.weight"})
+      hw.insert(hw.end(), sd[k].begin(), sd[k].end());
+    parts.push_back(hw);
+    const char* scal[] = {"dynamics.reward_conv.bias", "dynamics.fc_reward_hidden.weight",
+                          "dynamics.fc_reward_hidden.bias", "dynamics.fc_reward_output.weight",
+                          "dynamics.fc_reward_output.bias", "prediction.value_conv.bias",
+                          "prediction.value_fc.weight", "prediction.value_fc.bias",
+                          "prediction.policy_conv.bias", "prediction.pass_logit"};
+    for (const char* k : scal) parts.push_back(sd[k]);
+    std::vector<size_t> off;
+    size_t total = 0;
+    for (auto& p : parts) { off.push_back(total); total += (p.size() + 63) / 64 * 64; }
+    std::vector<float> blob(total, 0.f);
+    for (size_t i = 0; i < parts.size(); ++i) std::memcpy(blob.data() + off[i], parts[i].data(), parts[i].size() * 4);
+    if (total * 4 > d_w_bytes) {
+      if (d_w) (void)hipFree(d_w);
+      d_w = nullptr;
+      HIPCHK(hipMalloc(&d_w, total * 4));
+      d_w_bytes = total * 4;
+    }
+    HIPCHK(hipMemcpy(d_w, blob.data(), total * 4, hipMemcpyHostToDevice));
+    const float* b = d_w;
+    np.w_conv1 = b + off[0]; np.b_conv1 = b + off[1];
+    np.w_conv2 = b + off[2]; np.b_conv2 = b + off[3];
+    np.w_conv3 = b + off[4]; np.b_conv3 = b + off[5];
+    np.w_dyn = b + off[6]; np.b_dyn = b + off[7];
+    np.emb = b + off[8]; np.head_w = b + off[9];
+    np.hs.reward_b = b + off[10]; np.hs.fc1_w = b + off[11]; np.hs.fc1_b = b + off[12];
+    np.hs.fc2_w = b + off[13]; np.hs.fc2_b = b + off[14]; np.hs.value_b = b + off[15];
+    np.hs.vfc_w = b + off[16]; np.hs.vfc_b = b + off[17]; np.hs.policy_b = b + off[18];
+    np.hs.pass_logit = b + off[19];
+    dirty = false;
+    return MZGO_OK;
+  }
+
+  SearchParams search_params() const {
+    SearchParams sp;
+    sp.c_puct = cfg.c_puct; sp.discount = cfg.discount;
+    sp.dirichlet_alpha = cfg.dirichlet_alpha; sp.dirichlet_epsilon = cfg.dirichlet_epsilon;
+    sp.pass_epsilon = cfg.pass_epsilon; sp.num_simulations = S; sp.compat = cfg.compat;
+    sp.seed = cfg.seed;
+    return sp;
+  }
+};
+
+extern "C" {
+
+const char* mzgo_last_error(void) { return g_err.c_str(); }
+
+void mzgo_default_config(mzgo_config* c, int N) {
+  std::memset(c, 0, sizeof *c);
+  c->board_size = N;
+  c->latent_dim = 96;
+  c->num_games = 1;
+  c->num_simulations = 128;
+  c->max_moves = N * N;
+  c->compat = 0;
+  c->temperature_moves = 15;
+  c->c_puct = 2.5;
+  c->discount = 0.99;
+  c->dirichlet_alpha = 0.15;
+  c->dirichlet_epsilon = 0.02;
+  c->pass_epsilon = 0.01;
+  c->temperature = 1.0;
+  c->komi = 0.0;
+  c->seed = 1234;
+}
+
+int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
+  if (!cfg || !out) return fail(MZGO_EINVAL, "null argument");
+  *out = nullptr;
+  const int N = cfg->board_size, C = cfg->latent_dim;
+  const KernelSet* ks = find_kernels(N, C == 0 ? 96 : C);
+  if (!ks) return fail(MZGO_EINVAL, "unsupported board_size %d / latent_dim %d (built: N in {5,6,9,19}, C=96)", N, C);
+  if (cfg->num_games < 1) return fail(MZGO_EINVAL, "num_games must be >= 1");
+  if (C != 0 && cfg->num_simulations < 1) return fail(MZGO_EINVAL, "num_simulations must be >= 1");
+  if (cfg->compat != 0 && cfg->compat != 1) return fail(MZGO_EINVAL, "compat must be 0 or 1");
+  HIPCHK(hipSetDevice(cfg->device));
+  auto* e = new mzgo_engine();
+  e->cfg = *cfg;
+  e->ks = ks;
+  e->N = N; e->C = C; e->A = N * N + 1; e->CELLS = N * N; e->CS = (N * N + 15) / 16 * 16;
+  e->G = cfg->num_games;
+  e->S = C == 0 ? 0 : cfg->num_simulations;
+  e->M = cfg->max_moves > 0 ? cfg->max_moves : N * N;
+  e->cfg.max_moves = e->M;
+  e->spec = specs(C, e->A);
+  EngineArrays& E = e->E;
+  E.S = e->S;
+  E.max_moves = e->M;
+  const size_t G = e->G, n1 = (size_t)e->S + 1, A = e->A, CELLS = e->CELLS, M = e->M;
+  int rc = MZGO_OK;
+  auto chk = [&](int r) { if (r != MZGO_OK && rc == MZGO_OK) rc = r; };
+  if (C != 0) {
+    chk(e->alloc(&E.pool, G * n1 * (size_t)C * e->CS));
+    chk(e->alloc(&E.prior, G * n1 * A));
+    chk(e->alloc(&E.child, G * n1 * A));
+    chk(e->alloc(&E.visits, G * n1));
+    chk(e->alloc(&E.wsum, G * n1));
+    chk(e->alloc(&E.root_prior, G * A));
+    chk(e->alloc(&E.path, G * (n1 + 1)));
+    chk(e->alloc(&E.nodes, G));
+    chk(e->alloc(&E.rec_stones, G * M * CELLS));
+    chk(e->alloc(&E.rec_invd, G * M * CELLS));
+    chk(e->alloc(&E.rec_flags, G * M));
+    chk(e->alloc(&E.rec_action, G * M));
+    chk(e->alloc(&E.rec_value, G * M));
+    chk(e->alloc(&E.rec_policy, G * M * A));
+    chk(e->alloc(&E.rec_reward, G * M));
+  }
+  chk(e->alloc(&E.stones, G * CELLS));
+  chk(e->alloc(&E.invd, G * CELLS));
+  chk(e->alloc(&E.meta, G * 4));
+  chk(e->alloc(&E.game_len, G));
+  chk(e->alloc(&E.final_reward, G));
+  chk(e->alloc(&E.status, G));
+  chk(e->alloc(&E.counters, 4));
+  chk(e->alloc(&e->d_err, 1));
+  if (rc != MZGO_OK) { delete e; return rc; }
+  if (hipMemset(E.counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess) {
+    delete e;
+    return fail(MZGO_EHIP, "hipMemset failed");
+  }
+  hipError_t he = ks->board_reset(E, e->G, nullptr);
+  if (he == hipSuccess) he = hipDeviceSynchronize();
+  if (he != hipSuccess) { delete e; return fail(MZGO_EHIP, "board reset: %s", hipGetErrorString(he)); }
+  *out = e;
+  return MZGO_OK;
+}
+
+void mzgo_engine_destroy(mzgo_engine* e) { delete e; }
+
+int64_t mzgo_engine_device_bytes(const mzgo_engine* e) { return e ? e->bytes + (int64_t)e->d_w_bytes : 0; }
+
+int mzgo_set_weights(mzgo_engine* e, const char* key, const float* data, const int64_t* shape, int ndim) {
+  if (!e || !key || !data || (!shape && ndim > 0)) return fail(MZGO_EINVAL, "null argument");
+  for (const Spec& s : e->spec) {
+    if (std::strcmp(s.key, key) != 0) continue;
+    if ((int)s.shape.size() != ndim) return fail(MZGO_EINVAL, "'%s': expected %zu dims, got %d", key, s.shape.size(), ndim);
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) {
+      if (shape[i] != s.shape[i])
+        return fail(MZGO_EINVAL, "'%s': dim %d is %lld, expected %lld", key, i, (long long)shape[i], (long long)s.shape[i]);
+      n *= (size_t)shape[i];
+    }
+    e->sd[key].assign(data, data + n);
+    e->dirty = true;
+    return MZGO_OK;
+  }
+  return fail(MZGO_EINVAL, "unexpected key '%s' in state_dict", key);
+}
+
+int mzgo_weights_ready(const mzgo_engine* e) {
+  if (!e || e->C == 0) return 0;
+  for (const Spec& s : e->spec)
+    if (!e->sd.count(s.key)) return 0;
+  return 1;
+}
+
+int mzgo_initial_inference(mzgo_engine* e, const float* obs, int B, float* latent, float* value,
+                           float* logits, void* stream) {
+  if (!e || !obs || !latent || !value || !logits || B < 1) return fail(MZGO_EINVAL, "bad argument");
+  int rc = e->sync_weights();
+  if (rc) return rc;
+  HIPCHK(e->ks->initial_inference(e->np, obs, B, latent, value, logits, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_recurrent_inference(mzgo_engine* e, const float* latent, const int64_t* action, int B,
+                             float* next_latent, float* reward, float* value, float* logits, void* stream) {
+  if (!e || !latent || !action || !next_latent || !reward || !value || !logits || B < 1)
+    return fail(MZGO_EINVAL, "bad argument");
+  int rc = e->sync_weights();
+  if (rc) return rc;
+  HIPCHK(e->ks->recurrent_inference(e->np, latent, action, B, next_latent, reward, value, logits,
+                                    e->d_err, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_check_inference_errors(mzgo_engine* e, void* stream) {
+  if (!e) return fail(MZGO_EINVAL, "null engine");
+  int h = 0;
+  HIPCHK(hipMemcpyAsync(&h, e->d_err, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (h) {
+    HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(int), (hipStream_t)stream));
+    return fail(MZGO_EINVAL, "index out of range in self (action outside [0, %d))", e->A);
+  }
+  return MZGO_OK;
+}
+
+int mzgo_search(mzgo_engine* e, const float* root_obs, const double* noise, int G, int move_index,
+                int32_t* visits, double* value, void* stream) {
+  if (!e || !root_obs || G < 1 || G > e->G) return fail(MZGO_EINVAL, "bad argument (G=%d, engine has %d slots)", G, e ? e->G : 0);
+  int rc = e->sync_weights();
+  if (rc) return rc;
+  HIPCHK(e->ks->search(e->np, e->search_params(), e->E, root_obs, noise, G, e->cfg.game_base, move_index,
+                       visits, value, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_tree_export(mzgo_engine* e, int g, int32_t* n_nodes, int32_t* child, int32_t* visits,
+                     double* value_sum, float* prior, double* root_prior, void* stream) {
+  if (!e || e->C == 0 || g < 0 || g >= e->G) return fail(MZGO_EINVAL, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n1 = (size_t)e->S + 1, A = e->A;
+  int nn = 0;
+  HIPCHK(hipMemcpyAsync(&nn, e->E.nodes + g, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (n_nodes) *n_nodes = nn;
+  if (child) HIPCHK(hipMemcpyAsync(child, e->E.child + g * n1 * A, nn * A * 4, hipMemcpyDeviceToHost, s));
+  if (visits) HIPCHK(hipMemcpyAsync(visits, e->E.visits + g * n1, nn * 4, hipMemcpyDeviceToHost, s));
+  if (value_sum) HIPCHK(hipMemcpyAsync(value_sum, e->E.wsum + g * n1, nn * 8, hipMemcpyDeviceToHost, s));
+  if (prior) HIPCHK(hipMemcpyAsync(prior, e->E.prior + g * n1 * A, nn * A * 4, hipMemcpyDeviceToHost, s));
+  if (root_prior) HIPCHK(hipMemcpyAsync(root_prior, e->E.root_prior + g * A, A * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return MZGO_OK;
+}
+
+int mzgo_board_reset(mzgo_engine* e, void* stream) {
+  if (!e) return fail(MZGO_EINVAL, "null engine");
+  HIPCHK(e->ks->board_reset(e->E, e->G, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_board_step(mzgo_engine* e, const int32_t* actions, int32_t* status, double* winner, void* stream) {
+  if (!e || !actions) return fail(MZGO_EINVAL, "bad argument");
+  HIPCHK(e->ks->board_step(e->E, e->G, actions, status, winner, e->cfg.komi, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_board_planes(mzgo_engine* e, double* planes, void* stream) {
+  if (!e || !planes) return fail(MZGO_EINVAL, "bad argument");
+  HIPCHK(e->ks->board_planes(e->E, e->G, planes, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_board_set(mzgo_engine* e, int g, const int8_t* stones, const uint8_t* invd, const int32_t* meta,
+                   void* stream) {
+  if (!e || g < 0 || g >= e->G || !stones || !invd || !meta) return fail(MZGO_EINVAL, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(e->E.stones + (size_t)g * e->CELLS, stones, e->CELLS, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(e->E.invd + (size_t)g * e->CELLS, invd, e->CELLS, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(e->E.meta + (size_t)g * 4, meta, 16, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return MZGO_OK;
+}
+
+int mzgo_selfplay_reset(mzgo_engine* e, int epoch, void* stream) {
+  if (!e || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  e->epoch = epoch;
+  HIPCHK(e->ks->board_reset(e->E, e->G, s));
+  return MZGO_OK;
+}
+
+int mzgo_selfplay_move(mzgo_engine* e, void* stream) {
+  if (!e || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  int rc = e->sync_weights();
+  if (rc) return rc;
+  PlayParams pp;
+  pp.temperature = e->cfg.temperature;
+  pp.temperature_moves = e->cfg.temperature_moves;
+  pp.komi = e->cfg.komi;
+  pp.game_base = e->cfg.game_base;
+  pp.epoch = e->epoch;
+  pp.noise = e->noise;
+  HIPCHK(e->ks->selfplay_move(e->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_selfplay_inject_noise(mzgo_engine* e, const double* noise) {
+  if (!e) return fail(MZGO_EINVAL, "null engine");
+  e->noise = noise;
+  return MZGO_OK;
+}
+
+int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
+  if (!e || !out) return fail(MZGO_EINVAL, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long c[4] = {0, 0, 0, 0};
+  std::vector<int> st(e->G);
+  HIPCHK(hipMemcpyAsync(c, e->E.counters, sizeof c, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  int playing = 0;
+  for (int v : st) playing += v == 0;
+  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing;
+  return MZGO_OK;
+}
+
+int mzgo_records_export(mzgo_engine* e, int g, int32_t* length, int32_t* status, int8_t* stones,
+                        uint8_t* invd, uint8_t* flags, int32_t* action, double* value, double* policy,
+                        double* reward, double* final_reward, void* stream) {
+  if (!e || e->C == 0 || g < 0 || g >= e->G) return fail(MZGO_EINVAL, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  int meta[4], st = 0;
+  HIPCHK(hipMemcpyAsync(meta, e->E.meta + (size_t)g * 4, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&st, e->E.status + g, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const int L = meta[3];
+  if (length) *length = L;
+  if (status) *status = st;
+  const size_t M = e->M, CELLS = e->CELLS, A = e->A, base = (size_t)g * M;
+  if (L > 0) {
+    if (stones) HIPCHK(hipMemcpyAsync(stones, e->E.rec_stones + base * CELLS, L * CELLS, hipMemcpyDeviceToHost, s));
+    if (invd) HIPCHK(hipMemcpyAsync(invd, e->E.rec_invd + base * CELLS, L * CELLS, hipMemcpyDeviceToHost, s));
+    if (flags) HIPCHK(hipMemcpyAsync(flags, e->E.rec_flags + base, L, hipMemcpyDeviceToHost, s));
+    if (action) HIPCHK(hipMemcpyAsync(action, e->E.rec_action + base, L * 4, hipMemcpyDeviceToHost, s));
+    if (value) HIPCHK(hipMemcpyAsync(value, e->E.rec_value + base, L * 8, hipMemcpyDeviceToHost, s));
+    if (policy) HIPCHK(hipMemcpyAsync(policy, e->E.rec_policy + base * A, L * A * 8, hipMemcpyDeviceToHost, s));
+    if (reward) HIPCHK(hipMemcpyAsync(reward, e->E.rec_reward + base, L * 8, hipMemcpyDeviceToHost, s));
+  }
+  if (final_reward) HIPCHK(hipMemcpyAsync(final_reward, e->E.final_reward + g, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return MZGO_OK;
+}
+
+}  // extern "C"

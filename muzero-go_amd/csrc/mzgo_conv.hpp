@@ -1,0 +1,210 @@
+// mzgo_conv.hpp -- 3x3/pad-1 convolution of one board on one workgroup, on
+// fp32 MFMA (v_mfma_f32_16x16x4_f32), with the MuZero heads fused into the
+// epilogue.
+//
+// Implicit GEMM, transposed so the epilogue's head reductions run over the
+// accumulator's row index:
+//     out[cout][cell] = sum_k W[cout][k] * im2col[k][cell],  k = tap*CINP + cin
+// A operand (16 couts x 4 k)  : pre-packed weights streamed from L2
+//                               (layout written by pack_conv_weights, host side)
+// B operand (4 k x 16 cells)  : the input board staged in LDS as [cin][CPAD],
+//                               gathered per lane with the tap's cell offset
+// Each wave owns jobs of MG cout tiles x NG cell tiles (3x3 tiles of 16x16 at
+// C=96) so every A and B fragment feeds 3 MFMAs.
+//
+// Replaces the torch conv2d calls of self_play.py:66-74 (representation),
+// :80/:90 (dynamics) and the 1x1 head convs of :81, :100, :102.
+#pragma once
+#include "mzgo_common.hpp"
+
+namespace mzgo {
+
+// cout tiles per wave job for a conv with COUT outputs
+template <int COUT>
+struct ConvShape {
+  static constexpr int MT = COUT / 16;
+  static constexpr int MG = (MT % 3 == 0) ? 3 : ((MT % 4 == 0 && MT >= 8) ? 4 : 2);
+  static constexpr int MGP = (MG == 3) ? 4 : MG;  // packed floats per lane per k-step
+  static constexpr int NCOG = MT / MG;            // cout groups
+  static_assert(MT % MG == 0, "cout tiles");
+};
+
+template <int MGP>
+struct WFrag;
+template <> struct WFrag<2> { typedef float2 T; };
+template <> struct WFrag<4> { typedef float4 T; };
+
+__device__ inline float frag_get(const float2& v, int i) { return i == 0 ? v.x : v.y; }
+__device__ inline float frag_get(const float4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// Stage ``nch`` channels of a board held as [ch][src_stride] (f32, global) into
+// LDS [ch][CPAD]; optionally add emb[ch] to every cell (the action embedding
+// broadcast-add of self_play.py:87-89).  When src_stride == CS the copy moves
+// whole 16-byte chunks (pad cells included; the conv never reads them).
+template <class G>
+__device__ inline void stage_board(float* __restrict__ lds, const float* __restrict__ src,
+                                   int src_stride, int nch, const float* __restrict__ emb) {
+  if (src_stride == G::CS) {
+    constexpr int Q = G::CS / 4;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (int i = threadIdx.x; i < nch * Q; i += kThreads) {
+      int c = i / Q, q = i - c * Q;
+      float4 v = s4[c * Q + q];
+      if (emb) { float e = emb[c]; v.x += e; v.y += e; v.z += e; v.w += e; }
+      *reinterpret_cast<float4*>(lds + c * G::CPAD + q * 4) = v;
+    }
+  } else {
+    for (int i = threadIdx.x; i < nch * G::CELLS; i += kThreads) {
+      int c = i / G::CELLS, j = i - c * G::CELLS;
+      float v = src[c * src_stride + j];
+      if (emb) v += emb[c];
+      lds[c * G::CPAD + j] = v;
+    }
+  }
+}
+
+// Zero channels [c0, c1) of an LDS board (input padding of conv1: 6 -> 8 ch).
+template <class G>
+__device__ inline void zero_channels(float* lds, int c0, int c1) {
+  for (int i = threadIdx.x; i < (c1 - c0) * G::CPAD; i += kThreads) lds[c0 * G::CPAD + i] = 0.f;
+}
+
+// Head accumulation target: hp[cog][h][cell] in LDS, summed in fixed order later.
+template <class G>
+struct HeadPart {
+  float* base;  // [2][3][CS]
+  __device__ float* at(int cog, int h) const { return base + (cog * 3 + h) * G::CS; }
+};
+
+// The convolution.  lds_in: [CINP][CPAD] staged input.  wpk: packed weights.
+// out: [COUT][out_stride] (global), cells >= out_cells are not stored.
+// NH heads (0..3): head_w[h*COUT + cout]; partial sums land in hp.
+template <class G, int CIN, int COUT, int NH>
+__device__ inline void conv3x3(const float* __restrict__ lds_in, const float* __restrict__ wpk,
+                               const float* __restrict__ bias, float* __restrict__ out,
+                               int out_stride, int out_cells, const float* __restrict__ head_w,
+                               HeadPart<G> hp) {
+  typedef ConvShape<COUT> S;
+  constexpr int CINP = (CIN + 3) / 4 * 4;
+  constexpr int CQ = CINP / 4;                 // k-steps per tap
+  constexpr int KS = 9 * CQ;                   // k-steps
+  constexpr int MG = S::MG, MGP = S::MGP, NG = G::NG;
+  constexpr int JOBS = S::NCOG * G::NCG;
+  constexpr int PF = (CQ % 4 == 0) ? 4 : 2;    // A-fragment prefetch ring depth
+  constexpr int WSTEP = S::NCOG * 64 * MGP;    // floats per k-step in the packed weights
+  static_assert(CQ % PF == 0, "ring depth must divide the k-steps of a tap");
+  static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
+  typedef typename WFrag<MGP>::T wfrag;
+
+  const int lane = lane_id();
+  const int wave = wave_id();
+  const int kq = lane >> 4;       // k row of this lane inside a k-step (B operand)
+  const int col = lane & 15;      // cell column of this lane (B operand / accumulator)
+
+  for (int job = wave; job < JOBS; job += kWaves) {
+    const int cog = job % S::NCOG;
+    const int cg = job / S::NCOG;
+
+    // cell and (row, col) of this lane's column in each of the NG cell tiles
+    int cy[NG], cx[NG];
+    bool live[NG];
+#pragma unroll
+    for (int ni = 0; ni < NG; ++ni) {
+      int j = (cg * NG + ni) * 16 + col;
+      live[ni] = j < G::CELLS;
+      cy[ni] = j / G::N;
+      cx[ni] = j - cy[ni] * G::N;
+    }
+
+    f32x4 acc[MG][NG];
+#pragma unroll
+    for (int mi = 0; mi < MG; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NG; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const wfrag* wp = reinterpret_cast<const wfrag*>(wpk) + (cog * 64 + lane);
+    constexpr int WSTEP_F = WSTEP / MGP;  // in wfrag units
+    wfrag ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF - 1; ++p) ring[p] = wp[p * WSTEP_F];
+
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+      int off[NG];
+      bool ok[NG];
+#pragma unroll
+      for (int ni = 0; ni < NG; ++ni) {
+        int yy = cy[ni] + dy, xx = cx[ni] + dx;
+        ok[ni] = live[ni] && yy >= 0 && yy < G::N && xx >= 0 && xx < G::N;
+        off[ni] = ok[ni] ? yy * G::N + xx : 0;
+      }
+      const float* lrow = lds_in + kq * G::CPAD;
+#pragma unroll
+      for (int c4 = 0; c4 < CQ; ++c4) {
+        const int s = t * CQ + c4;
+        // prefetch the weights PF-1 k-steps ahead (a linear stream)
+        const int sp = s + PF - 1;
+        if (sp < KS) ring[(c4 + PF - 1) % PF] = wp[sp * WSTEP_F];
+        float b[NG];
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) {
+          float v = lrow[(c4 * 4) * G::CPAD + off[ni]];
+          b[ni] = ok[ni] ? v : 0.f;
+        }
+        const wfrag a = ring[c4 % PF];
+#pragma unroll
+        for (int mi = 0; mi < MG; ++mi) {
+          const float am = frag_get(a, mi);
+#pragma unroll
+          for (int ni = 0; ni < NG; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(am, b[ni], acc[mi][ni], 0, 0, 0);
+        }
+      }
+    }
+
+    // ---- epilogue: bias + ReLU, store, fused 1x1 heads ----
+    float hsum[NH > 0 ? NH : 1][NG];
+#pragma unroll
+    for (int h = 0; h < (NH > 0 ? NH : 1); ++h)
+#pragma unroll
+      for (int ni = 0; ni < NG; ++ni) hsum[h][ni] = 0.f;
+
+#pragma unroll
+    for (int mi = 0; mi < MG; ++mi) {
+      const int cout0 = (cog * MG + mi) * 16 + kq * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cout0 + r;
+        const float bb = bias[co];
+        float hw[NH > 0 ? NH : 1];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) hw[h] = head_w[h * COUT + co];
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) {
+          float v = acc[mi][ni][r] + bb;
+          v = v > 0.f ? v : 0.f;
+          const int cell = (cg * NG + ni) * 16 + col;
+          if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) hsum[h][ni] = __builtin_fmaf(hw[h], v, hsum[h][ni]);
+        }
+      }
+    }
+    if constexpr (NH > 0) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) {
+          float v = hsum[h][ni];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int cell = (cg * NG + ni) * 16 + col;
+          if (kq == 0 && cell < G::CS) hp.at(cog, h)[cell] = v;
+        }
+    }
+  }
+}
+
+}  // namespace mzgo

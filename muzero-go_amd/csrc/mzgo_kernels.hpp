@@ -1,0 +1,515 @@
+// mzgo_kernels.hpp -- the engine's kernels, templated on board size N and
+// latent_dim C and instantiated per (N, C) in mzgo_kernels_N*.hip.
+//
+// Every kernel runs one workgroup (4 waves) per game / batch element; games
+// never talk to each other, so there is no inter-workgroup synchronisation.
+#pragma once
+#include "mzgo_board.hpp"
+#include "mzgo_conv.hpp"
+#include "mzgo_search.hpp"
+
+namespace mzgo {
+
+// Network parameters on the device (packed by mzgo_capi.cpp).
+struct NetParams {
+  const float* w_conv1; const float* b_conv1;   // representation.conv1 (6 -> 64)
+  const float* w_conv2; const float* b_conv2;   // representation.conv2 (64 -> 64)
+  const float* w_conv3; const float* b_conv3;   // representation.conv3 (64 -> C)
+  const float* w_dyn;   const float* b_dyn;     // dynamics.conv (C -> C)
+  const float* emb;                             // dynamics.action_embedding [A][C]
+  const float* head_w;                          // [3][C]: reward_conv, value_conv, policy_conv
+  HeadScalars hs;
+};
+
+// Per-slot device state of an engine (sizes fixed at engine creation).
+struct EngineArrays {
+  int S;                 // simulations per move this engine was sized for
+  int max_moves;
+  // search state
+  float* pool;           // [G][S+1][C][CS] latents, node-indexed
+  float* prior;          // [G][S+1][A]
+  int* child;            // [G][S+1][A]
+  int* visits;           // [G][S+1]
+  double* wsum;          // [G][S+1]
+  double* root_prior;    // [G][A]
+  int* path;             // [G][S+2]
+  int* nodes;            // [G]  nodes used by the last search
+  // boards
+  int8_t* stones;        // [G][CELLS]
+  uint8_t* invd;         // [G][CELLS]
+  int* meta;             // [G][4] BoardMeta
+  // self-play records
+  int8_t* rec_stones;    // [G][M][CELLS]
+  uint8_t* rec_invd;     // [G][M][CELLS]
+  uint8_t* rec_flags;    // [G][M]   bit0 turn, bit1 passed, bit2 done
+  int* rec_action;       // [G][M]
+  double* rec_value;     // [G][M]
+  double* rec_policy;    // [G][M][A]
+  double* rec_reward;    // [G][M]
+  int* game_len;         // [G]
+  double* final_reward;  // [G]
+  int* status;           // [G]  0 playing, 1 finished, >=16 error
+  unsigned long long* counters;  // [4] 0: simulations run, 1: moves played, 2: games finished
+};
+
+template <class G>
+struct TreeViewOf {
+  __device__ static TreeView make(const EngineArrays& E, int g) {
+    const size_t n1 = (size_t)E.S + 1;
+    TreeView T;
+    T.prior = E.prior + (size_t)g * n1 * G::A;
+    T.child = E.child + (size_t)g * n1 * G::A;
+    T.visits = E.visits + (size_t)g * n1;
+    T.wsum = E.wsum + (size_t)g * n1;
+    T.root_prior = E.root_prior + (size_t)g * G::A;
+    T.path = E.path + (size_t)g * (n1 + 1);
+    return T;
+  }
+};
+
+// LDS of one game's workgroup.
+template <class G>
+struct Smem {
+  union alignas(16) {
+    float in[G::CINMAX * G::CPAD];                       // conv staging
+    struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
+  } u;
+  float hp[2 * 3 * G::CS];                               // head partials
+  TreeLds<G> t;
+  int8_t stone[G::CELLS];
+  uint8_t invd[G::CELLS];
+  int killed[4];
+  int misc[8];
+  int bc[8];                                             // broadcast slots
+};
+
+template <class G>
+__device__ inline BoardLds<G> board_lds(Smem<G>& sm) {
+  BoardLds<G> b;
+  b.stone = sm.stone; b.invd = sm.invd;
+  b.label = sm.u.scr.label; b.libs = sm.u.scr.libs; b.gsize = sm.u.scr.gsize;
+  b.killed = sm.killed; b.misc = sm.misc;
+  return b;
+}
+
+// ---------------------------------------------------------------------------
+// representation (self_play.py:70-74) + prediction heads (:104-113).
+// planes(c, cell) gives the f32 observation.  The latent is written to
+// ``lat`` ([C][lat_stride]), which also serves as scratch for conv1/conv2.
+// Leaves the logits in sm.t.logits and the value in sm.t.value.
+// ---------------------------------------------------------------------------
+template <class G, class PlaneFn>
+__device__ inline void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
+                                      int lat_stride) {
+  for (int i = threadIdx.x; i < 6 * G::CELLS; i += kThreads) {
+    const int c = i / G::CELLS, j = i - c * G::CELLS;
+    sm.u.in[c * G::CPAD + j] = planes(c, j);
+  }
+  zero_channels<G>(sm.u.in, 6, 8);
+  __syncthreads();
+  HeadPart<G> hp{sm.hp};
+  conv3x3<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, G::CELLS, nullptr, hp);
+  __syncthreads();
+  stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
+  __syncthreads();
+  conv3x3<G, 64, 64, 0>(sm.u.in, np.w_conv2, np.b_conv2, lat, lat_stride, G::CELLS, nullptr, hp);
+  __syncthreads();
+  stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
+  __syncthreads();
+  conv3x3<G, 64, G::C, 2>(sm.u.in, np.w_conv3, np.b_conv3, lat, lat_stride, G::CELLS,
+                          np.head_w + G::C, hp);
+  __syncthreads();
+  if (wave_id() == 0) finalize_heads<G>(sm.hp, false, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+  __syncthreads();
+}
+
+// dynamics (self_play.py:85-95) + prediction: ``src`` latent + emb[action]
+// -> ``dst`` latent; logits/reward/value left in sm.t.
+template <class G>
+__device__ inline void dynamics(Smem<G>& sm, const NetParams& np, const float* src, int src_stride,
+                                int action, float* dst, int dst_stride) {
+  stage_board<G>(sm.u.in, src, src_stride, G::C, np.emb + (size_t)action * G::C);
+  __syncthreads();
+  HeadPart<G> hp{sm.hp};
+  conv3x3<G, G::C, G::C, 3>(sm.u.in, np.w_dyn, np.b_dyn, dst, dst_stride,
+                            dst_stride == G::CS ? G::CS : G::CELLS, np.head_w, hp);
+  __syncthreads();
+  if (wave_id() == 0) finalize_heads<G>(sm.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Batched drop-in inference (self_play.py:121-128)
+// ---------------------------------------------------------------------------
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_initial_inference(NetParams np, const float* __restrict__ obs,
+                                                                 float* latent, float* value, float* logits) {
+  typedef Geo<N, C> G;
+  __shared__ Smem<G> sm;
+  const int b = blockIdx.x;
+  const float* o = obs + (size_t)b * 6 * G::CELLS;
+  float* lat = latent + (size_t)b * G::C * G::CELLS;
+  representation<G>(sm, np, [&](int c, int j) { return o[c * G::CELLS + j]; }, lat, G::CELLS);
+  for (int a = threadIdx.x; a < G::A; a += kThreads) logits[(size_t)b * G::A + a] = sm.t.logits[a];
+  if (threadIdx.x == 0) value[b] = sm.t.value;
+}
+
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
+                                                                   const int64_t* __restrict__ action,
+                                                                   float* next_latent, float* reward,
+                                                                   float* value, float* logits, int* err) {
+  typedef Geo<N, C> G;
+  __shared__ Smem<G> sm;
+  const int b = blockIdx.x;
+  int64_t a = action[b];
+  if (a < 0 || a >= G::A) {            // nn.Embedding would raise IndexError
+    if (threadIdx.x == 0) atomicOr(err, 1);
+    a = 0;
+  }
+  dynamics<G>(sm, np, latent + (size_t)b * G::C * G::CELLS, G::CELLS, (int)a,
+              next_latent + (size_t)b * G::C * G::CELLS, G::CELLS);
+  for (int i = threadIdx.x; i < G::A; i += kThreads) logits[(size_t)b * G::A + i] = sm.t.logits[i];
+  if (threadIdx.x == 0) { reward[b] = sm.t.reward; value[b] = sm.t.value; }
+}
+
+// ---------------------------------------------------------------------------
+// One full MCTS.run (self_play.py:148-237) for game slot g.
+// ---------------------------------------------------------------------------
+template <class G, class PlaneFn>
+__device__ inline void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                  const EngineArrays& E, int g, PlaneFn planes, const double* noise,
+                                  uint64_t key) {
+  const TreeView T = TreeViewOf<G>::make(E, g);
+  float* pool = E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS;
+  const size_t node_floats = (size_t)G::C * G::CS;
+  const int S = sp.num_simulations;
+
+  build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
+  tree_reset_root<G>(T);
+  representation<G>(sm, np, planes, pool, G::CS);        // root latent -> node 0
+  if (wave_id() == 0) root_priors<G>(sm.t, T, sp, noise, key);
+  __syncthreads();
+
+  int nodes = 1;
+  for (int sim = 0; sim < S; ++sim) {
+    if (wave_id() == 0) {
+      const int a = select_leaf<G>(sm.t, T, sp, key, sim);
+      if (lane_id() == 0) sm.t.action = a;
+    }
+    __syncthreads();
+    const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;
+    if (a < 0) {                                         // terminal leaf: backup 0 (:188-191)
+      if (threadIdx.x == 0) backup(T, depth, -1, 0.0);
+      __syncthreads();
+      continue;
+    }
+    const int nid = nodes++;
+    int* crow = T.child + (size_t)nid * G::A;
+    for (int i = threadIdx.x; i < G::A; i += kThreads) crow[i] = -1;
+    if (threadIdx.x == 0) { T.visits[nid] = 0; T.wsum[nid] = 0.0; }
+    dynamics<G>(sm, np, pool + (size_t)leaf * node_floats, G::CS, a, pool + (size_t)nid * node_floats, G::CS);
+    if (wave_id() == 0) {
+      child_priors<G>(sm.t, T.prior + (size_t)nid * G::A);
+      if (lane_id() == (a & 63)) T.child[(size_t)leaf * G::A + a] = nid;
+      if (lane_id() == 0) {
+        const double v = (double)sm.t.reward + sp.discount * (double)sm.t.value;
+        backup(T, depth, nid, v);
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) E.nodes[g] = nodes;
+  __syncthreads();
+}
+
+// root-child visit counts and root value of the finished search
+template <class G>
+__device__ inline void search_outputs(const EngineArrays& E, int g, int* out_visits, double* out_value) {
+  const TreeView T = TreeViewOf<G>::make(E, g);
+  for (int a = threadIdx.x; a < G::A; a += kThreads) {
+    const int c = T.child[a];
+    if (out_visits) out_visits[(size_t)g * G::A + a] = c >= 0 ? T.visits[c] : 0;
+  }
+  if (threadIdx.x == 0 && out_value) {
+    const int n = T.visits[0];
+    out_value[g] = n > 0 ? T.wsum[0] / (double)n : 0.0;
+  }
+}
+
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_search(NetParams np, SearchParams sp, EngineArrays E,
+                                                      const float* __restrict__ root_obs,
+                                                      const double* __restrict__ noise, int game_base,
+                                                      int move_index, int* out_visits, double* out_value) {
+  typedef Geo<N, C> G;
+  __shared__ Smem<G> sm;
+  const int g = blockIdx.x;
+  const float* o = root_obs + (size_t)g * 6 * G::CELLS;
+  const uint64_t key = stream_key(sp.seed, (uint32_t)(game_base + g), (uint32_t)move_index);
+  run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return o[c * G::CELLS + j]; },
+                noise ? noise + (size_t)g * G::A : nullptr, key);
+  search_outputs<G>(E, g, out_visits, out_value);
+}
+
+// ---------------------------------------------------------------------------
+// Boards
+// ---------------------------------------------------------------------------
+template <class G>
+__device__ inline void load_board(Smem<G>& sm, const EngineArrays& E, int g, BoardMeta& m) {
+  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+    sm.stone[c] = E.stones[(size_t)g * G::CELLS + c];
+    sm.invd[c] = E.invd[(size_t)g * G::CELLS + c];
+  }
+  const int* mm = E.meta + g * 4;
+  m.turn = mm[0]; m.passed = mm[1]; m.done = mm[2]; m.moves = mm[3];
+  __syncthreads();
+}
+
+template <class G>
+__device__ inline void store_board(Smem<G>& sm, const EngineArrays& E, int g, const BoardMeta& m) {
+  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+    E.stones[(size_t)g * G::CELLS + c] = sm.stone[c];
+    E.invd[(size_t)g * G::CELLS + c] = sm.invd[c];
+  }
+  if (threadIdx.x == 0) {
+    int* mm = E.meta + g * 4;
+    mm[0] = m.turn; mm[1] = m.passed; mm[2] = m.done; mm[3] = m.moves;
+  }
+}
+
+template <class G>
+__device__ inline float board_plane(const Smem<G>& sm, const BoardMeta& m, int c, int j) {
+  switch (c) {
+    case 0: return sm.stone[j] == 1 ? 1.f : 0.f;
+    case 1: return sm.stone[j] == 2 ? 1.f : 0.f;
+    case 2: return (float)m.turn;
+    case 3: return (float)sm.invd[j];
+    case 4: return (float)m.passed;
+    default: return (float)m.done;
+  }
+}
+
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_board_reset(EngineArrays E) {
+  typedef Geo<N, C> G;
+  const int g = blockIdx.x;
+  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+    E.stones[(size_t)g * G::CELLS + c] = 0;
+    E.invd[(size_t)g * G::CELLS + c] = 0;
+  }
+  if (threadIdx.x < 4) E.meta[g * 4 + threadIdx.x] = 0;
+  if (threadIdx.x == 0) { E.status[g] = 0; E.game_len[g] = 0; E.final_reward[g] = 0.0; }
+}
+
+// Step every slot with actions[g] >= 0 (gogame.next_state); status[g] gets a
+// BOARD_* code; winner[g] = GoEnv.winner() after the step (0 unless ended).
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_board_step(EngineArrays E, const int* __restrict__ actions,
+                                                          int* status, double* winner, double komi) {
+  typedef Geo<N, C> G;
+  __shared__ Smem<G> sm;
+  const int g = blockIdx.x;
+  const int a = actions[g];
+  if (a < 0) return;
+  BoardMeta m;
+  load_board<G>(sm, E, g, m);
+  BoardLds<G> b = board_lds<G>(sm);
+  const int st = board_step<G>(b, m, a);
+  __syncthreads();
+  if (st == BOARD_OK) store_board<G>(sm, E, g, m);
+  double w = 0.0;
+  if (st == BOARD_OK && m.done) w = board_winning<G>(b, komi);
+  if (threadIdx.x == 0) {
+    if (status) status[g] = st;
+    if (winner) winner[g] = w;
+  }
+}
+
+// f64 observation planes [G][6][CELLS] of the current boards (GoEnv state)
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_board_planes(EngineArrays E, double* planes) {
+  typedef Geo<N, C> G;
+  const int g = blockIdx.x;
+  const int* mm = E.meta + g * 4;
+  double* p = planes + (size_t)g * 6 * G::CELLS;
+  for (int j = threadIdx.x; j < G::CELLS; j += kThreads) {
+    const int s = E.stones[(size_t)g * G::CELLS + j];
+    p[j] = s == 1; p[G::CELLS + j] = s == 2; p[2 * G::CELLS + j] = mm[0];
+    p[3 * G::CELLS + j] = E.invd[(size_t)g * G::CELLS + j];
+    p[4 * G::CELLS + j] = mm[1]; p[5 * G::CELLS + j] = mm[2];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Action choice (MuZeroAgent.select_action, self_play.py:357-402).  Wave 0.
+// Writes the policy target to pol[A]; returns the action.
+// ---------------------------------------------------------------------------
+template <class G>
+__device__ inline int choose_action(TreeLds<G>& t, const TreeView& T, int compat, double temperature,
+                                    uint64_t key, double* pol) {
+  const int lane = lane_id();
+  // visit_counts * valid_mask (zeros under compat "reference", §0.6)
+  for (int a = lane; a < G::A; a += 64) {
+    double vc = 0.0;
+    if (compat == 1) { const int c = T.child[a]; vc = c >= 0 ? (double)T.visits[c] : 0.0; }
+    t.dbuf[a] = vc * mask_of<G>(t, a);
+  }
+  wave_lds_sync();
+  const double vsum = np_pairwise_sum<double, G::A>(t.dbuf);
+  double vcm[G::AP];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) { const int a = lane + 64 * j; vcm[j] = a < G::A ? t.dbuf[a] : 0.0; }
+  wave_lds_sync();
+  for (int a = lane; a < G::A; a += 64) t.dbuf[a] = mask_of<G>(t, a);
+  wave_lds_sync();
+  const double msum = np_pairwise_sum<double, G::A>(t.dbuf);
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    if (a < G::A) pol[a] = vsum > 0 ? vcm[j] / vsum : mask_of<G>(t, a) / msum;
+  }
+  const uint64_t h = draw(key, TAG_ACTION, 0);
+  int action = 0;
+  if (temperature == 0.0) {
+    if (vsum > 0) {                                    // argmax, first max wins
+      double bv = -1.0; int ba = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        if (a < G::A && (vcm[j] > bv || (vcm[j] == bv && a < ba))) { bv = vcm[j]; ba = a; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(bv, o); const int oa = __shfl_xor(ba, o);
+        if (ov > bv || (ov == bv && oa < ba)) { bv = ov; ba = oa; }
+      }
+      action = ba;
+    } else {                                           // random.choice(valid actions)
+      uint64_t vb[G::AP];
+      int nvalid = 0;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        vb[j] = __ballot(a < G::A && mask_of<G>(t, a) > 0);
+        nvalid += __popcll(vb[j]);
+      }
+      uint32_t k = randbelow(h, (uint32_t)nvalid);
+      action = -1;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const uint32_t c = __popcll(vb[j]);
+        if (action < 0 && k < c) {
+          uint64_t mm = vb[j];
+          for (uint32_t i = 0; i < k; ++i) mm &= mm - 1;
+          action = 64 * j + __ffsll((long long)mm) - 1;
+        } else if (action < 0) {
+          k -= c;
+        }
+      }
+    }
+  } else {
+    // probabilities = (vc**(1/T) * mask) / sum, or mask / sum(mask); then
+    // np.random.choice's inverse CDF on a cumulative sum
+    const double e = 1.0 / temperature;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      if (a < G::A) t.dbuf[a] = (e == 1.0 ? vcm[j] : pow(vcm[j], e)) * mask_of<G>(t, a);
+    }
+    wave_lds_sync();
+    const double ts = np_pairwise_sum<double, G::A>(t.dbuf);
+    wave_lds_sync();
+    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = ts > 0 ? t.dbuf[a] / ts : mask_of<G>(t, a) / msum;
+    wave_lds_sync();
+    if (lane == 0) {
+      double cdf = 0.0;
+      for (int a = 0; a < G::A; ++a) cdf += t.dbuf[a];
+      const double total = cdf;
+      const double u = u01(h);
+      double run = 0.0;
+      int idx = 0;
+      for (int a = 0; a < G::A; ++a) {
+        run += t.dbuf[a];
+        if (run / total <= u) idx = a + 1;
+      }
+      t.bcast = idx;
+    }
+    wave_lds_sync();
+    action = t.bcast;
+  }
+  return action;
+}
+
+// ---------------------------------------------------------------------------
+// One self-play move for every unfinished slot (run_self_play_game's loop
+// body, self_play.py:465-507): record the observation, search, choose, step
+// the board, record the result; finish the game on double pass or N*N moves.
+// ---------------------------------------------------------------------------
+struct PlayParams {
+  double temperature;     // 1.0
+  int temperature_moves;  // 15
+  double komi;            // 0
+  int game_base;          // global id of slot 0 (multi-GPU sharding)
+  int epoch;              // game generation (slot restarts), part of the RNG key
+  const double* noise;    // test hook: injected Dirichlet samples [G][M][A], or null
+};
+
+template <int N, int C>
+__global__ void __launch_bounds__(kThreads) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
+                                                             EngineArrays E) {
+  typedef Geo<N, C> G;
+  __shared__ Smem<G> sm;
+  const int g = blockIdx.x;
+  if (E.status[g] != 0) return;
+  BoardMeta m;
+  load_board<G>(sm, E, g, m);
+  const int mv = m.moves;
+  const size_t rec = (size_t)g * E.max_moves + mv;
+  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+    E.rec_stones[rec * G::CELLS + c] = sm.stone[c];
+    E.rec_invd[rec * G::CELLS + c] = sm.invd[c];
+  }
+  if (threadIdx.x == 0) E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
+
+  const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
+  const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
+  const BoardMeta m0 = m;
+  const double* noise = pp.noise ? pp.noise + ((size_t)g * E.max_moves + mv) * G::A : nullptr;
+  run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key);
+
+  const TreeView T = TreeViewOf<G>::make(E, g);
+  if (wave_id() == 0) {
+    const double temp = mv < pp.temperature_moves ? pp.temperature : 0.0;
+    const int a = choose_action<G>(sm.t, T, sp.compat, temp, key, E.rec_policy + rec * G::A);
+    if (lane_id() == 0) {
+      sm.bc[0] = a;
+      E.rec_action[rec] = a;
+      const int n = T.visits[0];
+      E.rec_value[rec] = n > 0 ? T.wsum[0] / (double)n : 0.0;
+    }
+  }
+  __syncthreads();
+  const int action = sm.bc[0];
+  BoardLds<G> b = board_lds<G>(sm);
+  const int st = board_step<G>(b, m, action);
+  __syncthreads();
+  double w = 0.0;
+  if (st == BOARD_OK && m.done) w = board_winning<G>(b, pp.komi);
+  store_board<G>(sm, E, g, m);
+  if (threadIdx.x == 0) {
+    E.rec_reward[rec] = w;
+    atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);
+    atomicAdd(&E.counters[1], 1ull);
+    if (st != BOARD_OK) {
+      E.status[g] = 16 + st;
+    } else if (m.done || m.moves >= E.max_moves) {
+      E.status[g] = 1;
+      E.game_len[g] = m.moves;
+      E.final_reward[g] = m.done ? w : 0.0;      // env.winner() is 0 unless ended
+      atomicAdd(&E.counters[2], 1ull);
+    }
+  }
+}
+
+}  // namespace mzgo

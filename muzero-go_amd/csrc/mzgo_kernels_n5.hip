@@ -1,0 +1,7 @@
+// Kernel instantiations for the 5x5 board (latent_dim 96, the reference's
+// self_play.py:21).  One translation unit per board size keeps builds parallel.
+#include "mzgo_dispatch.hpp"
+
+namespace mzgo {
+extern const KernelSet kernels_n5_c96 = Launch<5, 96>::table();
+}  // namespace mzgo

@@ -1,0 +1,375 @@
+// mzgo_search.hpp -- the MCTS of self_play.py as wave64 device code.
+//
+// One game's tree lives in HBM as structure-of-arrays node pools; wave 0 of
+// the game's workgroup walks it.  A lane owns actions a = lane + 64*j.
+//
+//   select_leaf       self_play.py:239-335  (unexpanded-first, min-max-Q PUCT)
+//   expand + backup   self_play.py:198-230, :337-343
+//   root_priors       self_play.py:151-182  (mask, normalise, Dirichlet, re-mask)
+//   choose_action     self_play.py:357-402  (compat "reference" and "fixed")
+//
+// Numerics follow numpy's dtype chain: root priors float64,
+// child priors float32 (softmax * root mask / numpy-ordered f32 sum), Q, U
+// and scores float64, backup value float64 = reward + 0.99 * value.
+#pragma once
+#include "mzgo_common.hpp"
+
+namespace mzgo {
+
+struct SearchParams {
+  double c_puct;            // 2.5 (self_play.py:143)
+  double discount;          // 0.99 (self_play.py:25)
+  double dirichlet_alpha;   // 0.15
+  double dirichlet_epsilon; // 0.02
+  double pass_epsilon;      // 0.01
+  int num_simulations;      // S
+  int compat;               // 0: reference (zero visit counts), 1: fixed
+  uint64_t seed;
+};
+
+// One game's tree (global memory).  Node 0 is the root; node ids grow by one
+// per expansion, so a search of S simulations uses at most S + 1 nodes.
+struct TreeView {
+  float* prior;       // [S+1][A] child priors of non-root nodes (f32)
+  int* child;         // [S+1][A] child node id, -1 = unexpanded
+  int* visits;        // [S+1]
+  double* wsum;       // [S+1]  value_sum
+  double* root_prior; // [A]    root child priors (f64)
+  int* path;          // [S+2]
+};
+
+// Per-game LDS block used by the tree phases.
+template <class G>
+struct TreeLds {
+  float logits[G::A];
+  float fbuf[G::A];
+  double dbuf[G::A];
+  uint8_t valid[G::A];     // valid_board (INVD == 0) for a < CELLS, 1 for pass
+  double pass_prior;       // 0.01 or 1.0
+  float reward, value;
+  int leaf, action, nid, depth, nodes, bcast;
+};
+
+template <class G>
+__device__ inline double mask_of(const TreeLds<G>& t, int a) {
+  return a < G::CELLS ? (t.valid[a] ? 1.0 : 0.0) : t.pass_prior;
+}
+
+// valid_mask from the INVD plane (self_play.py:152-158); call with all threads
+template <class G, class InvdFn>
+__device__ inline void build_mask(TreeLds<G>& t, double pass_epsilon, InvdFn invd) {
+  int any = 0;
+  for (int a = threadIdx.x; a < G::A; a += kThreads) {
+    uint8_t v = a < G::CELLS ? (invd(a) == 0 ? 1 : 0) : 1;
+    t.valid[a] = v;
+    any |= (a < G::CELLS) && v;
+  }
+  any = __syncthreads_or(any);
+  if (threadIdx.x == 0) t.pass_prior = any ? pass_epsilon : 1.0;
+  __syncthreads();
+}
+
+// softmax over t.logits -> t.fbuf (torch CPU order: exp(x - max) * (1/sum)).
+// Wave 0 only.
+template <class G>
+__device__ inline void softmax_wave(TreeLds<G>& t) {
+  const int lane = lane_id();
+  float m = -INFINITY;
+  for (int a = lane; a < G::A; a += 64) m = fmaxf(m, t.logits[a]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int a = lane; a < G::A; a += 64) { float e = expf(t.logits[a] - m); t.fbuf[a] = e; s += e; }
+  s = wave_sum(s);
+  const float inv = 1.0f / s;
+  for (int a = lane; a < G::A; a += 64) t.fbuf[a] = t.fbuf[a] * inv;
+}
+
+// Reward / value / logits from the fused head partials (self_play.py:91-94,
+// :105-112).  hp: [2][3][CS]; heads h0 (reward if has_reward), then value,
+// then policy.  hw: small head parameters (see HeadScalars).  Wave 0 only.
+struct HeadScalars {
+  const float* reward_b;    // [1]  reward_conv.bias
+  const float* fc1_w;       // [16] fc_reward_hidden.weight
+  const float* fc1_b;       // [16]
+  const float* fc2_w;       // [16] fc_reward_output.weight
+  const float* fc2_b;       // [1]
+  const float* value_b;     // [1]  value_conv.bias
+  const float* vfc_w;       // [1]  value_fc.weight
+  const float* vfc_b;       // [1]
+  const float* policy_b;    // [1]  policy_conv.bias
+  const float* pass_logit;  // [1]
+};
+
+template <class G>
+__device__ inline void finalize_heads(const float* hp, bool has_reward, const HeadScalars& hs,
+                                      float* logits, float* reward, float* value) {
+  const int lane = lane_id();
+  const int hv = has_reward ? 1 : 0, hpol = hv + 1;
+  auto head = [&](int h, int c) { return hp[h * G::CS + c] + hp[(3 + h) * G::CS + c]; };
+  const float vb = hs.value_b[0], pb = hs.policy_b[0];
+  float vs = 0.f, rs = 0.f;
+  const float rb = has_reward ? hs.reward_b[0] : 0.f;
+  for (int c = lane; c < G::CELLS; c += 64) {
+    vs += head(hv, c) + vb;
+    if (has_reward) rs += head(0, c) + rb;
+    logits[c] = head(hpol, c) + pb;
+  }
+  if (lane == 0) logits[G::CELLS] = hs.pass_logit[0];
+  vs = wave_sum(vs);
+  const float vmean = vs / (float)G::CELLS;
+  if (lane == 0) *value = vmean * hs.vfc_w[0] + hs.vfc_b[0];
+  if (has_reward) {
+    rs = wave_sum(rs);
+    const float rmean = rs / (float)G::CELLS;
+    float h = 0.f;
+    if (lane < 16) {
+      h = rmean * hs.fc1_w[lane] + hs.fc1_b[lane];
+      h = h > 0.f ? h : 0.f;
+      h = h * hs.fc2_w[lane];
+    }
+    h = wave_sum(h);
+    if (lane == 0) *reward = h + hs.fc2_b[0];
+  }
+}
+
+// Child priors of a new node (self_play.py:204-224): p = softmax * root mask,
+// normalised by numpy's f32 pairwise sum; entries with mask 0 are 0.  Wave 0.
+template <class G>
+__device__ inline void child_priors(TreeLds<G>& t, float* __restrict__ dst) {
+  const int lane = lane_id();
+  softmax_wave<G>(t);
+  for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
+  const float s = np_pairwise_sum<float, G::A>(t.fbuf);
+  if (s > 0.f) {
+    for (int a = lane; a < G::A; a += 64) {
+      const double m = mask_of<G>(t, a);
+      dst[a] = m > 0 ? t.fbuf[a] / s : 0.f;
+    }
+  } else {
+    // fallback of :215 (uniform over the mask; the reference's f64 here is
+    // stored as f32 -- unreachable unless every valid softmax entry underflows)
+    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = mask_of<G>(t, a);
+    const double ms = np_pairwise_sum<double, G::A>(t.dbuf);
+    for (int a = lane; a < G::A; a += 64) dst[a] = (float)(mask_of<G>(t, a) / ms);
+  }
+}
+
+// Gamma(alpha) by Marsaglia-Tsang with the alpha+1 boost, from the counter
+// stream (a << 16 | k).  Bounded: at most 64 proposals.
+__device__ inline double gamma_draw(uint64_t key, int a, double alpha) {
+  uint32_t k = 0;
+  auto U = [&]() { return u01(draw(key, TAG_DIRICHLET, ((uint64_t)a << 16) | (k++))); };
+  const double boost = pow(1.0 - U(), 1.0 / alpha);  // U in (0,1]
+  const double d = alpha + 1.0 - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+  for (int it = 0; it < 64; ++it) {
+    const double u1 = 1.0 - U(), u2 = U();
+    const double x = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+    double v = 1.0 + c * x;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    const double u = 1.0 - U();
+    if (log(u) < 0.5 * x * x + d - d * v + d * log(v)) return d * v * boost;
+  }
+  return d * boost;
+}
+
+// Root priors (self_play.py:151-182) into T.root_prior.  noise: injected
+// Dirichlet sample [A] (nullable: sample from the counter stream).  Wave 0.
+template <class G>
+__device__ inline void root_priors(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
+                                   const double* noise, uint64_t key) {
+  const int lane = lane_id();
+  softmax_wave<G>(t);
+  for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
+  const float s = np_pairwise_sum<float, G::A>(t.fbuf);
+  // Dirichlet sample d[a] -> dbuf (f64)
+  if (noise) {
+    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = noise[a];
+  } else {
+    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = gamma_draw(key, a, sp.dirichlet_alpha);
+    const double gs = np_pairwise_sum<double, G::A>(t.dbuf);
+    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = gs > 0 ? t.dbuf[a] / gs : 1.0 / G::A;
+  }
+  const double eps = sp.dirichlet_epsilon;
+  const float keep32 = (float)(1.0 - eps);   // Python float * f32 array -> f32 (NEP 50)
+  double q[G::AP];
+  if (s > 0.f) {
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      if (a < G::A) {
+        const float p = t.fbuf[a] / s;
+        q[j] = (double)(keep32 * p) + eps * t.dbuf[a];
+      }
+    }
+  } else {
+    // uniform-over-mask fallback (:164) is float64, so the noise mix is too
+    for (int a = lane; a < G::A; a += 64) t.fbuf[a] = 0.f;
+    double tmp[G::AP];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      tmp[j] = a < G::A ? mask_of<G>(t, a) : 0.0;
+    }
+    // sum of the mask in numpy order (reuse root_prior as scratch)
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) { const int a = lane + 64 * j; if (a < G::A) T.root_prior[a] = tmp[j]; }
+    __threadfence_block();
+    const double ms = np_pairwise_sum<double, G::A>(T.root_prior);
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      if (a < G::A) q[j] = (1.0 - eps) * (tmp[j] / ms) + eps * t.dbuf[a];
+    }
+  }
+  // policy *= valid_mask; normalise by numpy's f64 sum (:169-174)
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    if (a < G::A) { q[j] = q[j] * mask_of<G>(t, a); t.dbuf[a] = q[j]; }
+  }
+  const double s2 = np_pairwise_sum<double, G::A>(t.dbuf);
+  double ms = 0.0;
+  if (!(s2 > 0.0)) {
+    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = mask_of<G>(t, a);
+    ms = np_pairwise_sum<double, G::A>(t.dbuf);
+  }
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    if (a < G::A) {
+      const double m = mask_of<G>(t, a);
+      const double p = s2 > 0.0 ? q[j] / s2 : m / ms;
+      T.root_prior[a] = m > 0 ? p : 0.0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// select_leaf (self_play.py:239-335).  Wave 0.  Returns the action to expand
+// at t.leaf, or -1 when the walk ends at a terminal node (t.leaf).  The path
+// (node ids, root first) is written to T.path[0..depth].
+// ---------------------------------------------------------------------------
+template <class G>
+__device__ inline int select_leaf(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
+                                  uint64_t key, int sim) {
+  const int lane = lane_id();
+  int node = 0, depth = 0;
+  if (lane == 0) T.path[0] = 0;
+  for (int guard = 0; guard <= sp.num_simulations + 1; ++guard) {
+    const bool root = node == 0;
+    const int nvis = T.visits[node];
+    const int* ch_row = T.child + (size_t)node * G::A;
+    const float* pr_row = T.prior + (size_t)node * G::A;
+    double P[G::AP];
+    int ch[G::AP];
+    uint64_t anypos = 0, elig[G::AP], unexp[G::AP];
+    int n_unexp = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      const bool in = a < G::A;
+      P[j] = in ? (root ? T.root_prior[a] : (double)pr_row[a]) : 0.0;
+      ch[j] = in ? ch_row[a] : -1;
+      const bool pos = in && P[j] > 0.0;
+      const bool e = pos && mask_of<G>(t, a) > 0.0;
+      anypos |= __ballot(pos);
+      elig[j] = __ballot(e);
+      unexp[j] = __ballot(e && ch[j] < 0);
+      n_unexp += __popcll(unexp[j]);
+    }
+    uint64_t any_elig = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) any_elig |= elig[j];
+    if ((nvis > 0 && !anypos) || !any_elig) { t.leaf = node; t.depth = depth; return -1; }
+
+    if (n_unexp > 0) {
+      // random.choice over the ascending list of unexpanded eligible actions
+      uint32_t k = randbelow(draw(key, TAG_SELECT, (uint64_t)sim), (uint32_t)n_unexp);
+      int best = -1;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const uint32_t c = __popcll(unexp[j]);
+        if (best < 0 && k < c) {
+          uint64_t m = unexp[j];
+          for (uint32_t i = 0; i < k; ++i) m &= m - 1;  // drop the k lowest set bits
+          best = 64 * j + __ffsll((long long)m) - 1;
+        } else if (best < 0) {
+          k -= c;
+        }
+      }
+      t.leaf = node;
+      t.depth = depth;
+      return best;
+    }
+
+    // PUCT over the (all expanded) eligible children
+    double q[G::AP];
+    int n[G::AP];
+    double lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      q[j] = 0.0;
+      n[j] = 0;
+      if ((elig[j] >> lane) & 1ull) {
+        const int c = ch[j];
+        n[j] = T.visits[c];
+        q[j] = n[j] > 0 ? T.wsum[c] / (double)n[j] : 0.0;
+        lo = fmin(lo, q[j]);
+        hi = fmax(hi, q[j]);
+      }
+    }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    const double sq = sqrt((double)(nvis > 1 ? nvis : 1));
+    double best_s = -INFINITY;
+    int best_a = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      if ((elig[j] >> lane) & 1ull) {
+        const double qn = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
+        double u;
+        if (root) u = ((sp.c_puct * P[j]) * sq) / (double)(1 + n[j]);
+        else u = ((double)((float)sp.c_puct * (float)P[j]) * sq) / (double)(1 + n[j]);
+        const double sc = qn + u;
+        if (sc > best_s || (sc == best_s && a < best_a)) { best_s = sc; best_a = a; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_xor(best_s, o);
+      const int oa = __shfl_xor(best_a, o);
+      if (os > best_s || (os == best_s && oa < best_a)) { best_s = os; best_a = oa; }
+    }
+    if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return -1; }
+    const int nxt = T.child[(size_t)node * G::A + best_a];
+    depth += 1;
+    if (lane == 0) T.path[depth] = nxt;
+    node = nxt;
+  }
+  t.leaf = node;
+  t.depth = depth;
+  return -1;
+}
+
+// Backup along path[0..depth] (+ the new node nid if >= 0): leaf-most gets
+// +v, alternating sign upward (self_play.py:337-343).  Lane 0 of wave 0.
+__device__ inline void backup(const TreeView& T, int depth, int nid, double v) {
+  int i = 0;
+  if (nid >= 0) { T.visits[nid] += 1; T.wsum[nid] = T.wsum[nid] + v; i = 1; }
+  for (int d = depth; d >= 0; --d, ++i) {
+    const int node = T.path[d];
+    T.visits[node] += 1;
+    T.wsum[node] = T.wsum[node] + ((i & 1) ? -v : v);
+  }
+}
+
+// Reset a tree to a bare root (children unexpanded, stats zero).  All threads.
+template <class G>
+__device__ inline void tree_reset_root(const TreeView& T) {
+  for (int a = threadIdx.x; a < G::A; a += kThreads) T.child[a] = -1;
+  if (threadIdx.x == 0) { T.visits[0] = 0; T.wsum[0] = 0.0; }
+}
+
+}  // namespace mzgo

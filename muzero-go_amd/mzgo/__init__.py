@@ -1,0 +1,20 @@
+"""mzgo -- MI355X-native MuZero-Go self-play engine (host side).
+
+Drop-in counterparts of the reference's hot path (Sir-Teo/MuZero-Go
+self_play.py), all executed by libmzgo.so's HIP kernels:
+
+* ``MuZeroNet``   -- same parameters/state_dict keys; initial/recurrent inference on MFMA
+* ``MCTS``, ``MuZeroAgent`` -- device search (select / expand / backup kernels)
+* ``GoEnv``       -- GymGo rules as bit-exact integer kernels
+* ``SelfPlay``    -- G concurrent games per GPU, one fused kernel step per move
+* ``GameHistory``, ``save_batches`` -- the reference's record / pickle format
+"""
+from .engine import Engine, EngineConfig
+from .env import GoEnv
+from .net import MuZeroNet
+from .search import MCTS, MuZeroAgent
+from .selfplay import GameHistory, SelfPlay, history_from_device, save_batches
+from .weights import deterministic_state_dict
+
+__all__ = ["Engine", "EngineConfig", "GoEnv", "MuZeroNet", "MCTS", "MuZeroAgent", "SelfPlay",
+           "GameHistory", "history_from_device", "save_batches", "deterministic_state_dict"]

@@ -65,23 +65,8 @@ def _ref_net(sp, sd, C, A):
     return net.eval()
 
 
-def random_position(size, moves, seed):
-    """A legal position reached by uniform random play on the oracle board."""
-    from oracle import gogame
-    rng = np.random.default_rng(seed)
-    st = gogame.init_state(size)
-    for _ in range(moves):
-        if gogame.game_ended(st):
-            break
-        legal = np.flatnonzero(gogame.invalid_moves(st) == 0)
-        legal = legal[legal < size * size]          # keep the game going
-        if len(legal) == 0:
-            break
-        st = gogame.next_state(st, int(rng.choice(legal)))
-    return st
-
-
 def make_net(sp, N, B, C=96, seed=0):
+    from oracle.positions import random_position
     from oracle.weights import deterministic_state_dict
     A = N * N + 1
     sd = deterministic_state_dict(C, A, seed)
@@ -174,6 +159,7 @@ def _configure(sp, N, S):
 
 def make_mcts(sp, name, N, S, n_moves, seed=11, game=3, move=5, C=96):
     from oracle.mcts import tree_summary
+    from oracle.positions import random_position
     from oracle.weights import deterministic_state_dict
     A = N * N + 1
     _configure(sp, N, S)
