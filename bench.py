@@ -179,6 +179,14 @@ def main():
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                          "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3},
         }
+        prof = os.path.join(ROOT, "profiles", "latest_summary.json")
+        if os.path.exists(prof):
+            p = json.load(open(prof))
+            if p.get("workload") == out["config"]["workload"] and "k_selfplay_move" in p.get("kernel", ""):
+                # HBM bytes per launch from rocprofv3 PMC passes of this same command
+                # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/summarize_profile.py)
+                out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
+                out["roofline"]["traffic_source"] = f"profiles/{p['tag']}_summary.json"
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(N, C, S, args.cpu_budget)
         print(json.dumps(out))
