@@ -38,7 +38,7 @@ struct BoardLds {
 };
 
 template <class G>
-__device__ inline bool nbr(int c, int d, int& n) {
+__device__ __forceinline__ bool nbr(int c, int d, int& n) {
   const int r = c / G::N, col = c - r * G::N;
   switch (d) {
     case 0: if (r == 0) return false; n = c - G::N; return true;
@@ -51,7 +51,7 @@ __device__ inline bool nbr(int c, int d, int& n) {
 // label[c] = min cell index of c's 4-connected component of cells whose
 // class(c) is equal; -1 where class(c) == 0.
 template <class G, class ClassFn>
-__device__ inline void label_components(int* label, ClassFn cls) {
+__device__ __forceinline__ void label_components(int* label, ClassFn cls) {
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) label[c] = cls(c) ? c : -1;
   __syncthreads();
   for (int it = 0; it < G::CELLS + 2; ++it) {
@@ -75,7 +75,7 @@ __device__ inline void label_components(int* label, ClassFn cls) {
 
 // libs[g] = #distinct empty points adjacent to group g; gsize[g] = #stones
 template <class G>
-__device__ inline void count_liberties(BoardLds<G>& b, bool sizes) {
+__device__ __forceinline__ void count_liberties(BoardLds<G>& b, bool sizes) {
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) { b.libs[c] = 0; if (sizes) b.gsize[c] = 0; }
   __syncthreads();
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
@@ -101,7 +101,7 @@ __device__ inline void count_liberties(BoardLds<G>& b, bool sizes) {
 
 // INVD plane for the opponent of ``mover`` (state_utils.compute_invalid_moves)
 template <class G>
-__device__ inline void compute_invalid(BoardLds<G>& b, int mover, int ko) {
+__device__ __forceinline__ void compute_invalid(BoardLds<G>& b, int mover, int ko) {
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
     uint8_t inv;
     if (b.stone[c]) {
@@ -132,7 +132,7 @@ enum : int { BOARD_OK = 0, BOARD_ERR_DONE = 1, BOARD_ERR_INVALID = 2, BOARD_ERR_
 // gogame.next_state(state, action, canonical=False) on the LDS board.
 // Returns a BOARD_* status (uniform across the workgroup).
 template <class G>
-__device__ inline int board_step(BoardLds<G>& b, BoardMeta& m, int action) {
+__device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int action) {
   if (m.done) return BOARD_ERR_DONE;                 // GoEnv.step: assert not self.done
   if (action < 0 || action > G::CELLS) return BOARD_ERR_RANGE;
   const int player = m.turn;
@@ -195,7 +195,7 @@ __device__ inline int board_step(BoardLds<G>& b, BoardMeta& m, int action) {
 
 // gogame.winning: sign(black_area - white_area - komi), area (Tromp-Taylor).
 template <class G>
-__device__ inline double board_winning(BoardLds<G>& b, double komi) {
+__device__ __forceinline__ double board_winning(BoardLds<G>& b, double komi) {
   label_components<G>(b.label, [&](int c) { return b.stone[c] == 0 ? 1 : 0; });
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) { b.libs[c] = 0; b.gsize[c] = 0; }
   __syncthreads();

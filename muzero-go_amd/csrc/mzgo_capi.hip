@@ -262,6 +262,10 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   chk(e->alloc(&E.status, G));
   chk(e->alloc(&E.counters, 4));
   chk(e->alloc(&e->d_err, 1));
+#ifdef MZGO_STAMPS
+  chk(e->alloc(&E.stamps, G * kStampPhases));
+  if (E.stamps) (void)hipMemset(E.stamps, 0, G * kStampPhases * 8);
+#endif
   if (rc != MZGO_OK) { delete e; return rc; }
   if (hipMemset(E.counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess) {
@@ -462,5 +466,16 @@ int mzgo_records_export(mzgo_engine* e, int g, int32_t* length, int32_t* status,
   HIPCHK(hipStreamSynchronize(s));
   return MZGO_OK;
 }
+
+#ifdef MZGO_STAMPS
+// Diagnostic build only: copy (and zero) the per-slot phase cycle sums.
+int mzgo_debug_stamps(mzgo_engine* e, unsigned long long* host) {
+  if (!e || !e->E.stamps) return fail(MZGO_EINVAL, "no stamps");
+  const size_t n = (size_t)e->G * kStampPhases;
+  HIPCHK(hipMemcpy(host, e->E.stamps, n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(e->E.stamps, 0, n * 8));
+  return MZGO_OK;
+}
+#endif
 
 }  // extern "C"

@@ -42,49 +42,73 @@ struct Geo {
 // ---------------------------------------------------------------------------
 enum : uint32_t { TAG_SELECT = 1, TAG_DIRICHLET = 2, TAG_ACTION = 3, TAG_WEIGHT = 4 };
 
-__host__ __device__ inline uint64_t mix64(uint64_t z) {
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-__host__ __device__ inline uint64_t stream_key(uint64_t seed, uint32_t game, uint32_t move) {
+__host__ __device__ __forceinline__ uint64_t stream_key(uint64_t seed, uint32_t game, uint32_t move) {
   return mix64(mix64(seed) ^ ((uint64_t)game << 32 | (uint64_t)move));
 }
-__host__ __device__ inline uint64_t draw(uint64_t key, uint32_t tag, uint64_t idx) {
+__host__ __device__ __forceinline__ uint64_t draw(uint64_t key, uint32_t tag, uint64_t idx) {
   return mix64(key ^ ((uint64_t)(tag & 0xFF) << 56) ^ (idx & ((1ull << 56) - 1)));
 }
-__host__ __device__ inline double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
-__host__ __device__ inline uint32_t randbelow(uint64_t h, uint32_t n) {
+__host__ __device__ __forceinline__ double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+__host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
   return (uint32_t)(((h >> 32) * (uint64_t)n) >> 32);
 }
 
 // ---------------------------------------------------------------------------
+// Diagnostic phase stamps (only in a -DMZGO_STAMPS build; see
+// scripts/microbench.py).  Thread 0 of each workgroup adds shader-clock
+// deltas per phase into mzgo_stamps[block][phase].
+// ---------------------------------------------------------------------------
+constexpr int kStampPhases = 8;
+#ifdef MZGO_STAMPS
+struct Stamp {
+  unsigned long long* buf;
+  unsigned long long t;
+  __device__ explicit Stamp(unsigned long long* b) : buf(b) { t = __builtin_amdgcn_s_memtime(); }
+  __device__ void lap(int phase) {
+    unsigned long long now = __builtin_amdgcn_s_memtime();
+    if (buf && threadIdx.x == 0) buf[blockIdx.x * kStampPhases + phase] += now - t;
+    t = now;
+  }
+};
+#else
+struct Stamp {
+  __device__ explicit Stamp(unsigned long long*) {}
+  __device__ void lap(int) {}
+};
+#endif
+
+// ---------------------------------------------------------------------------
 // wave64 helpers
 // ---------------------------------------------------------------------------
-__device__ inline int lane_id() { return threadIdx.x & 63; }
-__device__ inline int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 // Order LDS traffic between lanes of one wave (no workgroup barrier needed).
-__device__ inline void wave_lds_sync() {
+__device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
 template <typename T>
-__device__ inline T wave_sum(T v) {
+__device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
 template <typename T>
-__device__ inline T wave_max(T v) {
+__device__ __forceinline__ T wave_max(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o); v = w > v ? w : v; }
   return v;
 }
 template <typename T>
-__device__ inline T wave_min(T v) {
+__device__ __forceinline__ T wave_min(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o); v = w < v ? w : v; }
   return v;
@@ -97,7 +121,7 @@ __device__ inline T wave_min(T v) {
 // so that normalised priors are bit-identical to the reference's.
 // ---------------------------------------------------------------------------
 template <typename T, int N>
-__device__ inline T np_pairwise_sum(const T* x) {
+__device__ __forceinline__ T np_pairwise_sum(const T* x) {
   wave_lds_sync();
   if constexpr (N < 8) {
     T r = (T)0;
@@ -125,6 +149,6 @@ __device__ inline T np_pairwise_sum(const T* x) {
 }
 
 // f32 result of numpy's in-place ``f32_array *= f64_array`` element
-__device__ inline float mul_f32_by_f64(float p, double m) { return (float)((double)p * m); }
+__device__ __forceinline__ float mul_f32_by_f64(float p, double m) { return (float)((double)p * m); }
 
 }  // namespace mzgo

@@ -34,8 +34,8 @@ struct WFrag;
 template <> struct WFrag<2> { typedef float2 T; };
 template <> struct WFrag<4> { typedef float4 T; };
 
-__device__ inline float frag_get(const float2& v, int i) { return i == 0 ? v.x : v.y; }
-__device__ inline float frag_get(const float4& v, int i) {
+__device__ __forceinline__ float frag_get(const float2& v, int i) { return i == 0 ? v.x : v.y; }
+__device__ __forceinline__ float frag_get(const float4& v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
@@ -44,7 +44,7 @@ __device__ inline float frag_get(const float4& v, int i) {
 // broadcast-add of self_play.py:87-89).  When src_stride == CS the copy moves
 // whole 16-byte chunks (pad cells included; the conv never reads them).
 template <class G>
-__device__ inline void stage_board(float* __restrict__ lds, const float* __restrict__ src,
+__device__ __forceinline__ void stage_board(float* __restrict__ lds, const float* __restrict__ src,
                                    int src_stride, int nch, const float* __restrict__ emb) {
   if (src_stride == G::CS) {
     constexpr int Q = G::CS / 4;
@@ -67,7 +67,7 @@ __device__ inline void stage_board(float* __restrict__ lds, const float* __restr
 
 // Zero channels [c0, c1) of an LDS board (input padding of conv1: 6 -> 8 ch).
 template <class G>
-__device__ inline void zero_channels(float* lds, int c0, int c1) {
+__device__ __forceinline__ void zero_channels(float* lds, int c0, int c1) {
   for (int i = threadIdx.x; i < (c1 - c0) * G::CPAD; i += kThreads) lds[c0 * G::CPAD + i] = 0.f;
 }
 
@@ -78,11 +78,13 @@ struct HeadPart {
   __device__ float* at(int cog, int h) const { return base + (cog * 3 + h) * G::CS; }
 };
 
-// The convolution.  lds_in: [CINP][CPAD] staged input.  wpk: packed weights.
+// The convolution with A fragments loaded straight from global memory (used
+// for representation.conv1, K = 72, where a weight ring does not pay).
+// lds_in: [CINP][CPAD] staged input.  wpk: packed weights.
 // out: [COUT][out_stride] (global), cells >= out_cells are not stored.
 // NH heads (0..3): head_w[h*COUT + cout]; partial sums land in hp.
 template <class G, int CIN, int COUT, int NH>
-__device__ inline void conv3x3(const float* __restrict__ lds_in, const float* __restrict__ wpk,
+__device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in, const float* __restrict__ wpk,
                                const float* __restrict__ bias, float* __restrict__ out,
                                int out_stride, int out_cells, const float* __restrict__ head_w,
                                HeadPart<G> hp) {
@@ -205,6 +207,238 @@ __device__ inline void conv3x3(const float* __restrict__ lds_in, const float* __
         }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// The main convolution: weights streamed global -> LDS by DMA
+// (global_load_lds_dwordx4) into a 3-slot ring, both MFMA operands read from
+// LDS.  One wave serves one cout group and JW cell groups, so a weight chunk
+// is fetched once per workgroup and each A fragment feeds MG x NG x JW MFMAs.
+//
+//   chunk c (KC k-steps, CHUNK bytes) lands in slot c % 3.  Every wave issues
+//   P 1-KiB pieces per chunk.  Iteration c: wait for own chunk-c pieces
+//   (s_waitcnt vmcnt(P) while chunk c+1 is in flight) -> s_barrier (all
+//   pieces landed, slot (c-1)%3 free) -> issue chunk c+2 -> compute chunk c.
+// ---------------------------------------------------------------------------
+template <class G, int COUT>
+struct Ring {
+  typedef ConvShape<COUT> S;
+  static constexpr int KSTEP_BYTES = S::NCOG * 64 * S::MGP * 4;
+  static constexpr int JPW = kWaves / S::NCOG;            // waves sharing one cout group
+  static constexpr int JW = (G::NCG + JPW - 1) / JPW;     // cell-group jobs per wave
+  static constexpr int P = JW >= 2 ? 1 : 2;               // 1-KiB DMA pieces per wave per chunk
+  static constexpr int CHUNK = P * kWaves * 1024;         // bytes per chunk
+  static constexpr int KC = CHUNK / KSTEP_BYTES;          // k-steps per chunk
+  static_assert(kWaves % S::NCOG == 0, "waves must split evenly over cout groups");
+};
+
+template <class G>
+struct RingBytes {
+  static constexpr int value = 3 * Ring<G, 64>::CHUNK > 3 * Ring<G, G::C>::CHUNK ? 3 * Ring<G, 64>::CHUNK
+                                                                                 : 3 * Ring<G, G::C>::CHUNK;
+};
+
+// 16 bytes per lane global -> LDS (global_load_lds_dwordx4).  Issued from
+// inline asm so that hipcc neither counts it nor guards every later ds_read
+// with s_waitcnt vmcnt(0) (it cannot tell which LDS bytes the DMA writes);
+// completion is tracked by hand with wait_vmcnt<N>() (MI355X guide §5.7).
+// lds_dst must be wave-uniform; the LDS destination is lds_dst + lane*16.
+__device__ __forceinline__ void dma16(const void* g, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds_dst)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+}
+
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int MGP>
+__device__ __forceinline__ typename WFrag<MGP>::T lds_frag(const float* p) {
+  return *reinterpret_cast<const typename WFrag<MGP>::T*>(p);
+}
+
+// hp_lds: head partials [2][3][CS]; written after a workgroup barrier, so it
+// may alias lds_in.  Returns with all waves synchronised.
+template <class G, int CIN, int COUT, int NH>
+__device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, const float* __restrict__ wpk,
+                                    const float* __restrict__ bias, float* __restrict__ out,
+                                    int out_stride, int out_cells, const float* __restrict__ head_w,
+                                    float* hp_lds) {
+  typedef ConvShape<COUT> S;
+  typedef Ring<G, COUT> R;
+  constexpr int CINP = (CIN + 3) / 4 * 4;
+  constexpr int CQ = CINP / 4;
+  constexpr int KS = 9 * CQ;
+  constexpr int KC = R::KC, NCH = KS / KC, JW = R::JW, NG = G::NG, MG = S::MG, MGP = S::MGP;
+  constexpr int CHUNK_F = R::CHUNK / 4;
+  static_assert(CQ % KC == 0, "a chunk must not straddle two taps");
+  static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
+  typedef typename WFrag<MGP>::T wfrag;
+
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());   // scalar: uniform branches
+  const int kq = lane >> 4, col = lane & 15;
+  const int cog = wave % S::NCOG;
+  const int cg0 = wave / S::NCOG;
+  const char* wsrc = reinterpret_cast<const char*>(wpk);
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+
+  auto issue = [&](int c) {
+#pragma unroll
+    for (int p = 0; p < R::P; ++p) {
+      const int piece = wave + kWaves * p;
+      dma16(wsrc + (size_t)c * R::CHUNK + piece * 1024 + lane * 16,
+            ring0 + (uint32_t)((c % 3) * R::CHUNK + piece * 1024));
+    }
+  };
+
+  int cy[JW][NG], cx[JW][NG];
+  bool live[JW][NG];
+#pragma unroll
+  for (int j = 0; j < JW; ++j)
+#pragma unroll
+    for (int ni = 0; ni < NG; ++ni) {
+      const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
+      live[j][ni] = cell < G::CELLS;
+      cy[j][ni] = cell / G::N;
+      cx[j][ni] = cell - cy[j][ni] * G::N;
+    }
+  // every job of every wave covers a real cell group unless NCG % JPW != 0
+  // (5x5, 6x6: JW == 1 and the second pair of waves has no cells)
+  constexpr bool ALL_LIVE = G::NCG % R::JPW == 0;
+  static_assert(ALL_LIVE || JW == 1, "partial job sets only with one job per wave");
+  bool jlive[JW];
+#pragma unroll
+  for (int j = 0; j < JW; ++j) jlive[j] = cg0 + j * R::JPW < G::NCG;
+
+  f32x4 acc[JW][MG][NG];
+#pragma unroll
+  for (int j = 0; j < JW; ++j)
+#pragma unroll
+    for (int mi = 0; mi < MG; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NG; ++ni) acc[j][mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (NCH > 1) issue(1);
+  int off[JW][NG];
+  bool ok[JW][NG];
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) wait_vmcnt<R::P>(); else wait_vmcnt<0>();
+    ring_barrier();
+    if (c + 2 < NCH) issue(c + 2);
+    const int s0 = c * KC;
+    const int t = s0 / CQ;
+    const int c40 = s0 - t * CQ;
+    if (c40 == 0) {
+      const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+#pragma unroll
+      for (int j = 0; j < JW; ++j)
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) {
+          const int yy = cy[j][ni] + dy, xx = cx[j][ni] + dx;
+          ok[j][ni] = live[j][ni] && yy >= 0 && yy < G::N && xx >= 0 && xx < G::N;
+          off[j][ni] = ok[j][ni] ? yy * G::N + xx : 0;
+        }
+    }
+    const float* slot = ring + (c % 3) * CHUNK_F + (cog * 64 + lane) * MGP;
+    const float* lrow = lds_in + (c40 * 4 + kq) * G::CPAD;
+    if (ALL_LIVE || jlive[0]) {                       // scalar; only 5x5 / 6x6 idle waves skip
+#pragma unroll
+      for (int kk = 0; kk < KC; ++kk) {
+        const wfrag a = lds_frag<MGP>(slot + kk * S::NCOG * 64 * MGP);
+        float b[JW][NG];
+#pragma unroll
+        for (int j = 0; j < JW; ++j)
+#pragma unroll
+          for (int ni = 0; ni < NG; ++ni) {
+            const float v = lrow[kk * 4 * G::CPAD + off[j][ni]];
+            b[j][ni] = ok[j][ni] ? v : 0.f;
+          }
+#pragma unroll
+        for (int j = 0; j < JW; ++j)
+#pragma unroll
+          for (int mi = 0; mi < MG; ++mi) {
+            const float am = frag_get(a, mi);
+#pragma unroll
+            for (int ni = 0; ni < NG; ++ni)
+              acc[j][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(am, b[j][ni], acc[j][mi][ni], 0, 0, 0);
+          }
+      }
+    }
+  }
+  __syncthreads();   // every wave is done with lds_in and the ring
+
+  // ---- epilogue: bias + ReLU, store, fused 1x1 heads ----
+  float hsum[NH > 0 ? NH : 1][JW][NG];
+#pragma unroll
+  for (int h = 0; h < (NH > 0 ? NH : 1); ++h)
+#pragma unroll
+    for (int j = 0; j < JW; ++j)
+#pragma unroll
+      for (int ni = 0; ni < NG; ++ni) hsum[h][j][ni] = 0.f;
+#pragma unroll
+  for (int mi = 0; mi < MG; ++mi) {
+    const int cout0 = (cog * MG + mi) * 16 + kq * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = cout0 + r;
+      const float bb = bias[co];
+      float hw[NH > 0 ? NH : 1];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hw[h] = head_w[h * COUT + co];
+#pragma unroll
+      for (int j = 0; j < JW; ++j) {
+        if (!jlive[j]) continue;
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) {
+          float v = acc[j][mi][ni][r] + bb;
+          v = v > 0.f ? v : 0.f;
+          const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
+          if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
+#pragma unroll
+          for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h], v, hsum[h][j][ni]);
+        }
+      }
+    }
+  }
+  if constexpr (NH > 0) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int j = 0; j < JW; ++j) {
+        if (!jlive[j]) continue;
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) {
+          float v = hsum[h][j][ni];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
+          if (kq == 0 && cell < G::CS) hp_lds[(cog * 3 + h) * G::CS + cell] = v;
+        }
+      }
+  }
+  __syncthreads();
 }
 
 }  // namespace mzgo

@@ -50,11 +50,12 @@ struct EngineArrays {
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
   unsigned long long* counters;  // [4] 0: simulations run, 1: moves played, 2: games finished
+  unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
 };
 
 template <class G>
 struct TreeViewOf {
-  __device__ static TreeView make(const EngineArrays& E, int g) {
+  __device__ __forceinline__ static TreeView make(const EngineArrays& E, int g) {
     const size_t n1 = (size_t)E.S + 1;
     TreeView T;
     T.prior = E.prior + (size_t)g * n1 * G::A;
@@ -72,9 +73,10 @@ template <class G>
 struct Smem {
   union alignas(16) {
     float in[G::CINMAX * G::CPAD];                       // conv staging
+    float hp[2 * 3 * G::CS];                             // head partials (after the conv loop)
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
   } u;
-  float hp[2 * 3 * G::CS];                               // head partials
+  alignas(16) float ring[RingBytes<G>::value / 4];       // weight DMA ring
   TreeLds<G> t;
   int8_t stone[G::CELLS];
   uint8_t invd[G::CELLS];
@@ -84,7 +86,7 @@ struct Smem {
 };
 
 template <class G>
-__device__ inline BoardLds<G> board_lds(Smem<G>& sm) {
+__device__ __forceinline__ BoardLds<G> board_lds(Smem<G>& sm) {
   BoardLds<G> b;
   b.stone = sm.stone; b.invd = sm.invd;
   b.label = sm.u.scr.label; b.libs = sm.u.scr.libs; b.gsize = sm.u.scr.gsize;
@@ -99,7 +101,7 @@ __device__ inline BoardLds<G> board_lds(Smem<G>& sm) {
 // Leaves the logits in sm.t.logits and the value in sm.t.value.
 // ---------------------------------------------------------------------------
 template <class G, class PlaneFn>
-__device__ inline void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
+__device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
                                       int lat_stride) {
   for (int i = threadIdx.x; i < 6 * G::CELLS; i += kThreads) {
     const int c = i / G::CELLS, j = i - c * G::CELLS;
@@ -107,34 +109,31 @@ __device__ inline void representation(Smem<G>& sm, const NetParams& np, PlaneFn 
   }
   zero_channels<G>(sm.u.in, 6, 8);
   __syncthreads();
-  HeadPart<G> hp{sm.hp};
-  conv3x3<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, G::CELLS, nullptr, hp);
+  HeadPart<G> hp{sm.u.hp};
+  conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, G::CELLS, nullptr, hp);
   __syncthreads();
   stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
   __syncthreads();
-  conv3x3<G, 64, 64, 0>(sm.u.in, np.w_conv2, np.b_conv2, lat, lat_stride, G::CELLS, nullptr, hp);
-  __syncthreads();
+  conv3x3_ring<G, 64, 64, 0>(sm.u.in, sm.ring, np.w_conv2, np.b_conv2, lat, lat_stride, G::CELLS,
+                             nullptr, sm.u.hp);
   stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
   __syncthreads();
-  conv3x3<G, 64, G::C, 2>(sm.u.in, np.w_conv3, np.b_conv3, lat, lat_stride, G::CELLS,
-                          np.head_w + G::C, hp);
-  __syncthreads();
-  if (wave_id() == 0) finalize_heads<G>(sm.hp, false, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+  conv3x3_ring<G, 64, G::C, 2>(sm.u.in, sm.ring, np.w_conv3, np.b_conv3, lat, lat_stride, G::CELLS,
+                               np.head_w + G::C, sm.u.hp);
+  if (wave_id() == 0) finalize_heads<G>(sm.u.hp, false, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
   __syncthreads();
 }
 
 // dynamics (self_play.py:85-95) + prediction: ``src`` latent + emb[action]
 // -> ``dst`` latent; logits/reward/value left in sm.t.
 template <class G>
-__device__ inline void dynamics(Smem<G>& sm, const NetParams& np, const float* src, int src_stride,
+__device__ __forceinline__ void dynamics(Smem<G>& sm, const NetParams& np, const float* src, int src_stride,
                                 int action, float* dst, int dst_stride) {
   stage_board<G>(sm.u.in, src, src_stride, G::C, np.emb + (size_t)action * G::C);
   __syncthreads();
-  HeadPart<G> hp{sm.hp};
-  conv3x3<G, G::C, G::C, 3>(sm.u.in, np.w_dyn, np.b_dyn, dst, dst_stride,
-                            dst_stride == G::CS ? G::CS : G::CELLS, np.head_w, hp);
-  __syncthreads();
-  if (wave_id() == 0) finalize_heads<G>(sm.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+  conv3x3_ring<G, G::C, G::C, 3>(sm.u.in, sm.ring, np.w_dyn, np.b_dyn, dst, dst_stride,
+                                 dst_stride == G::CS ? G::CS : G::CELLS, np.head_w, sm.u.hp);
+  if (wave_id() == 0) finalize_heads<G>(sm.u.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
   __syncthreads();
 }
 
@@ -177,7 +176,7 @@ __global__ void __launch_bounds__(kThreads) k_recurrent_inference(NetParams np, 
 // One full MCTS.run (self_play.py:148-237) for game slot g.
 // ---------------------------------------------------------------------------
 template <class G, class PlaneFn>
-__device__ inline void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+__device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                   const EngineArrays& E, int g, PlaneFn planes, const double* noise,
                                   uint64_t key) {
   const TreeView T = TreeViewOf<G>::make(E, g);
@@ -192,12 +191,14 @@ __device__ inline void run_search(Smem<G>& sm, const NetParams& np, const Search
   __syncthreads();
 
   int nodes = 1;
+  Stamp st(E.stamps);
   for (int sim = 0; sim < S; ++sim) {
     if (wave_id() == 0) {
       const int a = select_leaf<G>(sm.t, T, sp, key, sim);
       if (lane_id() == 0) sm.t.action = a;
     }
     __syncthreads();
+    st.lap(0);
     const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;
     if (a < 0) {                                         // terminal leaf: backup 0 (:188-191)
       if (threadIdx.x == 0) backup(T, depth, -1, 0.0);
@@ -208,16 +209,27 @@ __device__ inline void run_search(Smem<G>& sm, const NetParams& np, const Search
     int* crow = T.child + (size_t)nid * G::A;
     for (int i = threadIdx.x; i < G::A; i += kThreads) crow[i] = -1;
     if (threadIdx.x == 0) { T.visits[nid] = 0; T.wsum[nid] = 0.0; }
-    dynamics<G>(sm, np, pool + (size_t)leaf * node_floats, G::CS, a, pool + (size_t)nid * node_floats, G::CS);
+    stage_board<G>(sm.u.in, pool + (size_t)leaf * node_floats, G::CS, G::C, np.emb + (size_t)a * G::C);
+    __syncthreads();
+    st.lap(1);
+    conv3x3_ring<G, G::C, G::C, 3>(sm.u.in, sm.ring, np.w_dyn, np.b_dyn, pool + (size_t)nid * node_floats,
+                                   G::CS, G::CS, np.head_w, sm.u.hp);
+    st.lap(2);
+    if (wave_id() == 0) finalize_heads<G>(sm.u.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+    __syncthreads();
+    st.lap(3);
     if (wave_id() == 0) {
       child_priors<G>(sm.t, T.prior + (size_t)nid * G::A);
       if (lane_id() == (a & 63)) T.child[(size_t)leaf * G::A + a] = nid;
-      if (lane_id() == 0) {
-        const double v = (double)sm.t.reward + sp.discount * (double)sm.t.value;
-        backup(T, depth, nid, v);
-      }
     }
     __syncthreads();
+    st.lap(4);
+    if (threadIdx.x == 0) {
+      const double v = (double)sm.t.reward + sp.discount * (double)sm.t.value;
+      backup(T, depth, nid, v);
+    }
+    __syncthreads();
+    st.lap(5);
   }
   if (threadIdx.x == 0) E.nodes[g] = nodes;
   __syncthreads();
@@ -225,7 +237,7 @@ __device__ inline void run_search(Smem<G>& sm, const NetParams& np, const Search
 
 // root-child visit counts and root value of the finished search
 template <class G>
-__device__ inline void search_outputs(const EngineArrays& E, int g, int* out_visits, double* out_value) {
+__device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int* out_visits, double* out_value) {
   const TreeView T = TreeViewOf<G>::make(E, g);
   for (int a = threadIdx.x; a < G::A; a += kThreads) {
     const int c = T.child[a];
@@ -256,7 +268,7 @@ __global__ void __launch_bounds__(kThreads) k_search(NetParams np, SearchParams 
 // Boards
 // ---------------------------------------------------------------------------
 template <class G>
-__device__ inline void load_board(Smem<G>& sm, const EngineArrays& E, int g, BoardMeta& m) {
+__device__ __forceinline__ void load_board(Smem<G>& sm, const EngineArrays& E, int g, BoardMeta& m) {
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
     sm.stone[c] = E.stones[(size_t)g * G::CELLS + c];
     sm.invd[c] = E.invd[(size_t)g * G::CELLS + c];
@@ -267,7 +279,7 @@ __device__ inline void load_board(Smem<G>& sm, const EngineArrays& E, int g, Boa
 }
 
 template <class G>
-__device__ inline void store_board(Smem<G>& sm, const EngineArrays& E, int g, const BoardMeta& m) {
+__device__ __forceinline__ void store_board(Smem<G>& sm, const EngineArrays& E, int g, const BoardMeta& m) {
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
     E.stones[(size_t)g * G::CELLS + c] = sm.stone[c];
     E.invd[(size_t)g * G::CELLS + c] = sm.invd[c];
@@ -279,7 +291,7 @@ __device__ inline void store_board(Smem<G>& sm, const EngineArrays& E, int g, co
 }
 
 template <class G>
-__device__ inline float board_plane(const Smem<G>& sm, const BoardMeta& m, int c, int j) {
+__device__ __forceinline__ float board_plane(const Smem<G>& sm, const BoardMeta& m, int c, int j) {
   switch (c) {
     case 0: return sm.stone[j] == 1 ? 1.f : 0.f;
     case 1: return sm.stone[j] == 2 ? 1.f : 0.f;
@@ -346,7 +358,7 @@ __global__ void __launch_bounds__(kThreads) k_board_planes(EngineArrays E, doubl
 // Writes the policy target to pol[A]; returns the action.
 // ---------------------------------------------------------------------------
 template <class G>
-__device__ inline int choose_action(TreeLds<G>& t, const TreeView& T, int compat, double temperature,
+__device__ __forceinline__ int choose_action(TreeLds<G>& t, const TreeView& T, int compat, double temperature,
                                     uint64_t key, double* pol) {
   const int lane = lane_id();
   // visit_counts * valid_mask (zeros under compat "reference", §0.6)

@@ -51,13 +51,13 @@ struct TreeLds {
 };
 
 template <class G>
-__device__ inline double mask_of(const TreeLds<G>& t, int a) {
+__device__ __forceinline__ double mask_of(const TreeLds<G>& t, int a) {
   return a < G::CELLS ? (t.valid[a] ? 1.0 : 0.0) : t.pass_prior;
 }
 
 // valid_mask from the INVD plane (self_play.py:152-158); call with all threads
 template <class G, class InvdFn>
-__device__ inline void build_mask(TreeLds<G>& t, double pass_epsilon, InvdFn invd) {
+__device__ __forceinline__ void build_mask(TreeLds<G>& t, double pass_epsilon, InvdFn invd) {
   int any = 0;
   for (int a = threadIdx.x; a < G::A; a += kThreads) {
     uint8_t v = a < G::CELLS ? (invd(a) == 0 ? 1 : 0) : 1;
@@ -72,7 +72,7 @@ __device__ inline void build_mask(TreeLds<G>& t, double pass_epsilon, InvdFn inv
 // softmax over t.logits -> t.fbuf (torch CPU order: exp(x - max) * (1/sum)).
 // Wave 0 only.
 template <class G>
-__device__ inline void softmax_wave(TreeLds<G>& t) {
+__device__ __forceinline__ void softmax_wave(TreeLds<G>& t) {
   const int lane = lane_id();
   float m = -INFINITY;
   for (int a = lane; a < G::A; a += 64) m = fmaxf(m, t.logits[a]);
@@ -101,7 +101,7 @@ struct HeadScalars {
 };
 
 template <class G>
-__device__ inline void finalize_heads(const float* hp, bool has_reward, const HeadScalars& hs,
+__device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward, const HeadScalars& hs,
                                       float* logits, float* reward, float* value) {
   const int lane = lane_id();
   const int hv = has_reward ? 1 : 0, hpol = hv + 1;
@@ -135,7 +135,7 @@ __device__ inline void finalize_heads(const float* hp, bool has_reward, const He
 // Child priors of a new node (self_play.py:204-224): p = softmax * root mask,
 // normalised by numpy's f32 pairwise sum; entries with mask 0 are 0.  Wave 0.
 template <class G>
-__device__ inline void child_priors(TreeLds<G>& t, float* __restrict__ dst) {
+__device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst) {
   const int lane = lane_id();
   softmax_wave<G>(t);
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
@@ -156,7 +156,7 @@ __device__ inline void child_priors(TreeLds<G>& t, float* __restrict__ dst) {
 
 // Gamma(alpha) by Marsaglia-Tsang with the alpha+1 boost, from the counter
 // stream (a << 16 | k).  Bounded: at most 64 proposals.
-__device__ inline double gamma_draw(uint64_t key, int a, double alpha) {
+__device__ __forceinline__ double gamma_draw(uint64_t key, int a, double alpha) {
   uint32_t k = 0;
   auto U = [&]() { return u01(draw(key, TAG_DIRICHLET, ((uint64_t)a << 16) | (k++))); };
   const double boost = pow(1.0 - U(), 1.0 / alpha);  // U in (0,1]
@@ -176,7 +176,7 @@ __device__ inline double gamma_draw(uint64_t key, int a, double alpha) {
 // Root priors (self_play.py:151-182) into T.root_prior.  noise: injected
 // Dirichlet sample [A] (nullable: sample from the counter stream).  Wave 0.
 template <class G>
-__device__ inline void root_priors(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
+__device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
                                    const double* noise, uint64_t key) {
   const int lane = lane_id();
   softmax_wave<G>(t);
@@ -251,7 +251,7 @@ __device__ inline void root_priors(TreeLds<G>& t, const TreeView& T, const Searc
 // (node ids, root first) is written to T.path[0..depth].
 // ---------------------------------------------------------------------------
 template <class G>
-__device__ inline int select_leaf(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
+__device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
                                   uint64_t key, int sim) {
   const int lane = lane_id();
   int node = 0, depth = 0;
@@ -355,7 +355,7 @@ __device__ inline int select_leaf(TreeLds<G>& t, const TreeView& T, const Search
 
 // Backup along path[0..depth] (+ the new node nid if >= 0): leaf-most gets
 // +v, alternating sign upward (self_play.py:337-343).  Lane 0 of wave 0.
-__device__ inline void backup(const TreeView& T, int depth, int nid, double v) {
+__device__ __forceinline__ void backup(const TreeView& T, int depth, int nid, double v) {
   int i = 0;
   if (nid >= 0) { T.visits[nid] += 1; T.wsum[nid] = T.wsum[nid] + v; i = 1; }
   for (int d = depth; d >= 0; --d, ++i) {
@@ -367,7 +367,7 @@ __device__ inline void backup(const TreeView& T, int depth, int nid, double v) {
 
 // Reset a tree to a bare root (children unexpanded, stats zero).  All threads.
 template <class G>
-__device__ inline void tree_reset_root(const TreeView& T) {
+__device__ __forceinline__ void tree_reset_root(const TreeView& T) {
   for (int a = threadIdx.x; a < G::A; a += kThreads) T.child[a] = -1;
   if (threadIdx.x == 0) { T.visits[0] = 0; T.wsum[0] = 0.0; }
 }

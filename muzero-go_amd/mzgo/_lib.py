@@ -12,7 +12,7 @@ import os
 
 import torch  # noqa: F401  (must precede loading libmzgo.so)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmzgo.so")
+LIB_PATH = os.environ.get("MZGO_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmzgo.so")
 
 MZGO_OK, MZGO_EINVAL, MZGO_EHIP, MZGO_ENOWEIGHTS, MZGO_EASSERT = 0, -1, -2, -3, -4
 

@@ -1,0 +1,92 @@
+"""Per-phase timing of the engine's kernels (development aid).
+
+Times, for 9x9 / C=96 / G=256: batched recurrent_inference (the dynamics conv
++ heads alone), initial_inference, one full search (k_search, S sims) and one
+self-play move, each averaged over several launches with HIP events.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "muzero-go_amd")]
+import torch  # noqa: E402
+
+import mzgo  # noqa: E402
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    N = int(os.environ.get("N", 9))
+    G = int(os.environ.get("G", 256))
+    S = int(os.environ.get("S", 200))
+    C = 96
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda().eval()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    eng = net.engine()
+    lat = torch.rand(G, C, N, N, device="cuda")
+    act = torch.randint(0, A, (G,), device="cuda")
+    obs = (torch.rand(G, 6, N, N, device="cuda") < 0.2).float()
+    obs[:, 2:] = 0
+    out = {}
+    out["recurrent_inference_ms"] = timeit(lambda: eng.recurrent_inference(lat, act))
+    out["initial_inference_ms"] = timeit(lambda: eng.initial_inference(obs))
+    seng = net.engine(num_games=G, num_simulations=S)
+    out["search_ms"] = timeit(lambda: seng.search(obs), reps=3)
+    sp = mzgo.SelfPlay(net, G, S)
+    sp.reset()
+    out["selfplay_move_ms"] = timeit(sp.move, reps=3)
+    out["per_sim_us"] = out["search_ms"] / S * 1e3
+    out["conv_share"] = out["recurrent_inference_ms"] / (out["search_ms"] / S)
+    print(json.dumps({"N": N, "G": G, "S": S, **out}))
+
+
+if __name__ == "__main__" and not os.environ.get("STAMPS"):
+    main()
+
+
+def stamps_report():
+    """With MZGO_LIB=...libmzgo_stamps.so: cycles per simulation by phase."""
+    import ctypes
+
+    import numpy as np
+    from mzgo import _lib
+    N = int(os.environ.get("N", 9))
+    G = int(os.environ.get("G", 256))
+    S = int(os.environ.get("S", 200))
+    C, A = 96, N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda().eval()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    seng = net.engine(num_games=G, num_simulations=S)
+    obs = torch.zeros(G, 6, N, N)
+    fn = _lib.lib.mzgo_debug_stamps
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
+    buf = np.zeros((G, 8), np.uint64)
+    seng.search(obs)
+    torch.cuda.synchronize()
+    fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
+    ms = timeit(lambda: seng.search(obs), reps=1)
+    fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))
+    names = ["select", "stage", "conv", "heads", "priors", "backup", "-", "-"]
+    per_sim = buf.astype(np.float64).mean(0) / (2 * S)            # warm-up call inside timeit + 1 rep
+    total = per_sim[:6].sum()
+    print(json.dumps({"N": N, "G": G, "S": S, "search_ms": ms,
+                      "cycles_per_sim": {n: round(float(v)) for n, v in zip(names, per_sim) if n != "-"},
+                      "share": {n: round(float(v / total), 3) for n, v in zip(names, per_sim) if n != "-"},
+                      "implied_clock_GHz": total * S / (ms * 1e6)}))
+
+
+if os.environ.get("STAMPS"):
+    stamps_report()
