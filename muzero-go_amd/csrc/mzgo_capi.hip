@@ -72,7 +72,11 @@ std::vector<Spec> specs(int C, int A) {
 // conv weight W[cout][cin][3][3] -> MFMA A-fragment order of mzgo_conv.hpp:
 // packed[((s * NCOG + cog) * 64 + lane) * MGP + mi] with k-step s = tap*CQ + c4,
 // cout = (cog*MG + mi)*16 + (lane & 15), cin = c4*4 + (lane >> 4).
-std::vector<float> pack_conv(const float* W, int COUT, int CIN) {
+// With cog_major the layout is packed[((cog * KS + s) * 64 + lane) * MGP + mi]
+// (one contiguous stream per cout group, for the per-wave DMA rings of
+// conv3x3_ring); otherwise [((s * NCOG + cog) * 64 + lane) * MGP + mi]
+// (conv3x3_direct).
+std::vector<float> pack_conv(const float* W, int COUT, int CIN, bool cog_major) {
   const int CINP = (CIN + 3) / 4 * 4, CQ = CINP / 4, KS = 9 * CQ;
   const int MT = COUT / 16;
   const int MG = (MT % 3 == 0) ? 3 : ((MT % 4 == 0 && MT >= 8) ? 4 : 2);
@@ -86,7 +90,8 @@ std::vector<float> pack_conv(const float* W, int COUT, int CIN) {
           const int cout = (cog * MG + mi) * 16 + (lane & 15);
           const int cin = c4 * 4 + (lane >> 4);
           const float v = cin < CIN ? W[(((size_t)cout * CIN + cin) * 3 + ky) * 3 + kx] : 0.f;
-          out[(((size_t)s * NCOG + cog) * 64 + lane) * MGP + mi] = v;
+          const size_t frag = cog_major ? (size_t)cog * KS + s : (size_t)s * NCOG + cog;
+          out[(frag * 64 + lane) * MGP + mi] = v;
         }
   }
   return out;
@@ -133,13 +138,13 @@ struct mzgo_engine {
     for (const Spec& s : spec)
       if (!sd.count(s.key)) return fail(MZGO_ENOWEIGHTS, "missing weight '%s'", s.key);
     std::vector<std::vector<float>> parts;
-    parts.push_back(pack_conv(sd["representation.conv1.weight"].data(), 64, 6));
+    parts.push_back(pack_conv(sd["representation.conv1.weight"].data(), 64, 6, false));
     parts.push_back(sd["representation.conv1.bias"]);
-    parts.push_back(pack_conv(sd["representation.conv2.weight"].data(), 64, 64));
+    parts.push_back(pack_conv(sd["representation.conv2.weight"].data(), 64, 64, true));
     parts.push_back(sd["representation.conv2.bias"]);
-    parts.push_back(pack_conv(sd["representation.conv3.weight"].data(), C, 64));
+    parts.push_back(pack_conv(sd["representation.conv3.weight"].data(), C, 64, true));
     parts.push_back(sd["representation.conv3.bias"]);
-    parts.push_back(pack_conv(sd["dynamics.conv.weight"].data(), C, C));
+    parts.push_back(pack_conv(sd["dynamics.conv.weight"].data(), C, C, true));
     parts.push_back(sd["dynamics.conv.bias"]);
     parts.push_back(sd["dynamics.action_embedding.weight"]);
     std::vector<float> hw;

@@ -210,32 +210,38 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
 }
 
 // ---------------------------------------------------------------------------
-// The main convolution: weights streamed global -> LDS by DMA
-// (global_load_lds_dwordx4) into a 3-slot ring, both MFMA operands read from
-// LDS.  One wave serves one cout group and JW cell groups, so a weight chunk
-// is fetched once per workgroup and each A fragment feeds MG x NG x JW MFMAs.
+// The main convolution: each wave streams ITS OWN cout group's weights
+// global -> LDS by DMA (global_load_lds_dwordx4) into a private NSLOT-slot
+// ring, so the k-loop has no workgroup barrier at all -- only per-wave
+// s_waitcnt vmcnt (MI355X guide: LDS-DMA data is visible to the issuing wave
+// after its own vmcnt wait).  Both MFMA operands come from LDS.  One wave
+// serves one cout group and JW cell groups, so each A fragment feeds
+// MG x NG x JW MFMAs.  Weights are packed cog-major ([cog][k-step][lane][MGP],
+// pack_conv(..., cog_major=true)) so a wave's stream is contiguous.
 //
-//   chunk c (KC k-steps, CHUNK bytes) lands in slot c % 3.  Every wave issues
-//   P 1-KiB pieces per chunk.  Iteration c: wait for own chunk-c pieces
-//   (s_waitcnt vmcnt(P) while chunk c+1 is in flight) -> s_barrier (all
-//   pieces landed, slot (c-1)%3 free) -> issue chunk c+2 -> compute chunk c.
+//   wave chunk c (KC k-steps, SLOT bytes) lands in slot c % NSLOT.
+//   iteration c: issue chunk c+NSLOT-1 (into the slot read in iteration c-1)
+//   -> wait until chunk c landed -> compute chunk c.
 // ---------------------------------------------------------------------------
 template <class G, int COUT>
 struct Ring {
   typedef ConvShape<COUT> S;
-  static constexpr int KSTEP_BYTES = S::NCOG * 64 * S::MGP * 4;
-  static constexpr int JPW = kWaves / S::NCOG;            // waves sharing one cout group
-  static constexpr int JW = (G::NCG + JPW - 1) / JPW;     // cell-group jobs per wave
-  static constexpr int P = JW >= 2 ? 1 : 2;               // 1-KiB DMA pieces per wave per chunk
-  static constexpr int CHUNK = P * kWaves * 1024;         // bytes per chunk
-  static constexpr int KC = CHUNK / KSTEP_BYTES;          // k-steps per chunk
+  static constexpr int KSTEP_BYTES = 64 * S::MGP * 4;       // one cog, one k-step (1 KiB or 512 B)
+  static constexpr int JPW = kWaves / S::NCOG;              // waves sharing one cout group
+  static constexpr int JW = (G::NCG + JPW - 1) / JPW;       // cell-group jobs per wave
+  static constexpr int KC = JW >= 2 ? (1024 / KSTEP_BYTES) : 8;   // k-steps per chunk
+  static constexpr int NSLOT = JW >= 2 ? 2 : 3;
+  static constexpr int SLOT = KC * KSTEP_BYTES;             // bytes per slot (multiple of 1 KiB)
+  static constexpr int NGLDS = SLOT / 1024;                 // DMA instructions per chunk
   static_assert(kWaves % S::NCOG == 0, "waves must split evenly over cout groups");
+  static_assert(SLOT % 1024 == 0, "slots are whole 1-KiB DMA pieces");
 };
 
 template <class G>
 struct RingBytes {
-  static constexpr int value = 3 * Ring<G, 64>::CHUNK > 3 * Ring<G, G::C>::CHUNK ? 3 * Ring<G, 64>::CHUNK
-                                                                                 : 3 * Ring<G, G::C>::CHUNK;
+  static constexpr int a = Ring<G, 64>::NSLOT * Ring<G, 64>::SLOT;
+  static constexpr int b = Ring<G, G::C>::NSLOT * Ring<G, G::C>::SLOT;
+  static constexpr int value = kWaves * (a > b ? a : b);   // all waves' private rings
 };
 
 // 16 bytes per lane global -> LDS (global_load_lds_dwordx4).  Issued from
@@ -262,14 +268,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-}
-
-__device__ __forceinline__ void ring_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
 template <int MGP>
@@ -283,14 +283,14 @@ template <class G, int CIN, int COUT, int NH>
 __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, const float* __restrict__ wpk,
                                     const float* __restrict__ bias, float* __restrict__ out,
                                     int out_stride, int out_cells, const float* __restrict__ head_w,
-                                    float* hp_lds) {
+                                    float* hp_lds, Stamp* st = nullptr) {
   typedef ConvShape<COUT> S;
   typedef Ring<G, COUT> R;
   constexpr int CINP = (CIN + 3) / 4 * 4;
   constexpr int CQ = CINP / 4;
   constexpr int KS = 9 * CQ;
   constexpr int KC = R::KC, NCH = KS / KC, JW = R::JW, NG = G::NG, MG = S::MG, MGP = S::MGP;
-  constexpr int CHUNK_F = R::CHUNK / 4;
+  constexpr int NSLOT = R::NSLOT;
   static_assert(CQ % KC == 0, "a chunk must not straddle two taps");
   static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
   typedef typename WFrag<MGP>::T wfrag;
@@ -300,17 +300,16 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
   const int kq = lane >> 4, col = lane & 15;
   const int cog = wave % S::NCOG;
   const int cg0 = wave / S::NCOG;
-  const char* wsrc = reinterpret_cast<const char*>(wpk);
-  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  // this wave's contiguous weight stream and private ring
+  const char* wsrc = reinterpret_cast<const char*>(wpk) + (size_t)cog * KS * R::KSTEP_BYTES + lane * 16;
+  float* myring = ring + wave * (RingBytes<G>::value / kWaves / 4);
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(myring));
 
-  auto issue = [&](int c) {
-#pragma unroll
-    for (int p = 0; p < R::P; ++p) {
-      const int piece = wave + kWaves * p;
-      dma16(wsrc + (size_t)c * R::CHUNK + piece * 1024 + lane * 16,
-            ring0 + (uint32_t)((c % 3) * R::CHUNK + piece * 1024));
-    }
-  };
+  // every job of every wave covers a real cell group unless NCG % JPW != 0
+  // (5x5, 6x6: JW == 1 and the second pair of waves has no cells)
+  constexpr bool ALL_LIVE = G::NCG % R::JPW == 0;
+  static_assert(ALL_LIVE || JW == 1, "partial job sets only with one job per wave");
+  const bool active = ALL_LIVE || cg0 < G::NCG;                // scalar
 
   int cy[JW][NG], cx[JW][NG];
   bool live[JW][NG];
@@ -323,13 +322,6 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
       cy[j][ni] = cell / G::N;
       cx[j][ni] = cell - cy[j][ni] * G::N;
     }
-  // every job of every wave covers a real cell group unless NCG % JPW != 0
-  // (5x5, 6x6: JW == 1 and the second pair of waves has no cells)
-  constexpr bool ALL_LIVE = G::NCG % R::JPW == 0;
-  static_assert(ALL_LIVE || JW == 1, "partial job sets only with one job per wave");
-  bool jlive[JW];
-#pragma unroll
-  for (int j = 0; j < JW; ++j) jlive[j] = cg0 + j * R::JPW < G::NCG;
 
   f32x4 acc[JW][MG][NG];
 #pragma unroll
@@ -339,42 +331,65 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
 #pragma unroll
       for (int ni = 0; ni < NG; ++ni) acc[j][mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0);
-  if (NCH > 1) issue(1);
-  int off[JW][NG];
-  bool ok[JW][NG];
-  for (int c = 0; c < NCH; ++c) {
-    if (c + 1 < NCH) wait_vmcnt<R::P>(); else wait_vmcnt<0>();
-    ring_barrier();
-    if (c + 2 < NCH) issue(c + 2);
-    const int s0 = c * KC;
-    const int t = s0 / CQ;
-    const int c40 = s0 - t * CQ;
-    if (c40 == 0) {
-      const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+  if (active) {
+    auto issue = [&](int c) {
+#ifndef MZGO_DIAG_NODMA
 #pragma unroll
-      for (int j = 0; j < JW; ++j)
+      for (int p = 0; p < R::NGLDS; ++p)
+        dma16(wsrc + (size_t)c * R::SLOT + p * 1024, ring0 + (uint32_t)((c % NSLOT) * R::SLOT + p * 1024));
+#endif
+    };
 #pragma unroll
-        for (int ni = 0; ni < NG; ++ni) {
-          const int yy = cy[j][ni] + dy, xx = cx[j][ni] + dx;
-          ok[j][ni] = live[j][ni] && yy >= 0 && yy < G::N && xx >= 0 && xx < G::N;
-          off[j][ni] = ok[j][ni] ? yy * G::N + xx : 0;
-        }
-    }
-    const float* slot = ring + (c % 3) * CHUNK_F + (cog * 64 + lane) * MGP;
-    const float* lrow = lds_in + (c40 * 4 + kq) * G::CPAD;
-    if (ALL_LIVE || jlive[0]) {                       // scalar; only 5x5 / 6x6 idle waves skip
-#pragma unroll
-      for (int kk = 0; kk < KC; ++kk) {
-        const wfrag a = lds_frag<MGP>(slot + kk * S::NCOG * 64 * MGP);
-        float b[JW][NG];
+    for (int c = 0; c < NSLOT - 1; ++c)
+      if (c < NCH) issue(c);
+    int off[JW][NG];
+    bool ok[JW][NG];
+    for (int c = 0; c < NCH; ++c) {
+      if (c + NSLOT - 1 < NCH) {
+        issue(c + NSLOT - 1);
+        wait_vmcnt<R::NGLDS * (NSLOT - 1)>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      const int s0 = c * KC;
+      const int t = s0 / CQ;
+      const int c40 = s0 - t * CQ;
+      if (c40 == 0) {
+        const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
 #pragma unroll
         for (int j = 0; j < JW; ++j)
 #pragma unroll
           for (int ni = 0; ni < NG; ++ni) {
-            const float v = lrow[kk * 4 * G::CPAD + off[j][ni]];
-            b[j][ni] = ok[j][ni] ? v : 0.f;
+            const int yy = cy[j][ni] + dy, xx = cx[j][ni] + dx;
+            ok[j][ni] = live[j][ni] && yy >= 0 && yy < G::N && xx >= 0 && xx < G::N;
+            off[j][ni] = ok[j][ni] ? yy * G::N + xx : 0;
           }
+      }
+      const float* slot = myring + (c % NSLOT) * (R::SLOT / 4) + lane * MGP;
+      const float* lrow = lds_in + (c40 * 4 + kq) * G::CPAD;
+      // operands of k-step kk+1 are fetched before the MFMAs of k-step kk
+      // (one wave per SIMD: LDS latency must hide behind this wave's MFMAs)
+      wfrag a_nx = lds_frag<MGP>(slot);
+      float b_nx[JW][NG];
+#pragma unroll
+      for (int j = 0; j < JW; ++j)
+#pragma unroll
+        for (int ni = 0; ni < NG; ++ni) b_nx[j][ni] = lrow[off[j][ni]];
+#pragma unroll
+      for (int kk = 0; kk < KC; ++kk) {
+        const wfrag a = a_nx;
+        float b[JW][NG];
+#pragma unroll
+        for (int j = 0; j < JW; ++j)
+#pragma unroll
+          for (int ni = 0; ni < NG; ++ni) b[j][ni] = ok[j][ni] ? b_nx[j][ni] : 0.f;
+        if (kk + 1 < KC) {
+          a_nx = lds_frag<MGP>(slot + (kk + 1) * 64 * MGP);
+#pragma unroll
+          for (int j = 0; j < JW; ++j)
+#pragma unroll
+            for (int ni = 0; ni < NG; ++ni) b_nx[j][ni] = lrow[(kk + 1) * 4 * G::CPAD + off[j][ni]];
+        }
 #pragma unroll
         for (int j = 0; j < JW; ++j)
 #pragma unroll
@@ -387,7 +402,9 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
       }
     }
   }
-  __syncthreads();   // every wave is done with lds_in and the ring
+  if (st) st->lap(6);
+  __syncthreads();   // every wave is done with lds_in
+  if (st) st->lap(7);
 
   // ---- epilogue: bias + ReLU, store, fused 1x1 heads ----
   float hsum[NH > 0 ? NH : 1][JW][NG];
@@ -397,46 +414,46 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
     for (int j = 0; j < JW; ++j)
 #pragma unroll
       for (int ni = 0; ni < NG; ++ni) hsum[h][j][ni] = 0.f;
+  if (active) {
 #pragma unroll
-  for (int mi = 0; mi < MG; ++mi) {
-    const int cout0 = (cog * MG + mi) * 16 + kq * 4;
+    for (int mi = 0; mi < MG; ++mi) {
+      const int cout0 = (cog * MG + mi) * 16 + kq * 4;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = cout0 + r;
-      const float bb = bias[co];
-      float hw[NH > 0 ? NH : 1];
+      for (int r = 0; r < 4; ++r) {
+        const int co = cout0 + r;
+        const float bb = bias[co];
+        float hw[NH > 0 ? NH : 1];
 #pragma unroll
-      for (int h = 0; h < NH; ++h) hw[h] = head_w[h * COUT + co];
+        for (int h = 0; h < NH; ++h) hw[h] = head_w[h * COUT + co];
 #pragma unroll
-      for (int j = 0; j < JW; ++j) {
-        if (!jlive[j]) continue;
+        for (int j = 0; j < JW; ++j) {
 #pragma unroll
-        for (int ni = 0; ni < NG; ++ni) {
-          float v = acc[j][mi][ni][r] + bb;
-          v = v > 0.f ? v : 0.f;
-          const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
-          if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
+          for (int ni = 0; ni < NG; ++ni) {
+            float v = acc[j][mi][ni][r] + bb;
+            v = v > 0.f ? v : 0.f;
+            const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
+            if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
 #pragma unroll
-          for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h], v, hsum[h][j][ni]);
+            for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h], v, hsum[h][j][ni]);
+          }
         }
       }
     }
-  }
-  if constexpr (NH > 0) {
+    if constexpr (NH > 0) {
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+      for (int h = 0; h < NH; ++h)
 #pragma unroll
-      for (int j = 0; j < JW; ++j) {
-        if (!jlive[j]) continue;
+        for (int j = 0; j < JW; ++j) {
 #pragma unroll
-        for (int ni = 0; ni < NG; ++ni) {
-          float v = hsum[h][j][ni];
-          v += __shfl_xor(v, 16);
-          v += __shfl_xor(v, 32);
-          const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
-          if (kq == 0 && cell < G::CS) hp_lds[(cog * 3 + h) * G::CS + cell] = v;
+          for (int ni = 0; ni < NG; ++ni) {
+            float v = hsum[h][j][ni];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
+            if (kq == 0 && cell < G::CS) hp_lds[(cog * 3 + h) * G::CS + cell] = v;
+          }
         }
-      }
+    }
   }
   __syncthreads();
 }

@@ -141,7 +141,7 @@ __device__ __forceinline__ void dynamics(Smem<G>& sm, const NetParams& np, const
 // Batched drop-in inference (self_play.py:121-128)
 // ---------------------------------------------------------------------------
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_initial_inference(NetParams np, const float* __restrict__ obs,
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_initial_inference(NetParams np, const float* __restrict__ obs,
                                                                  float* latent, float* value, float* logits) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(kThreads) k_initial_inference(NetParams np, co
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
                                                                    const int64_t* __restrict__ action,
                                                                    float* next_latent, float* reward,
                                                                    float* value, float* logits, int* err) {
@@ -213,7 +213,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
     __syncthreads();
     st.lap(1);
     conv3x3_ring<G, G::C, G::C, 3>(sm.u.in, sm.ring, np.w_dyn, np.b_dyn, pool + (size_t)nid * node_floats,
-                                   G::CS, G::CS, np.head_w, sm.u.hp);
+                                   G::CS, G::CS, np.head_w, sm.u.hp, &st);
     st.lap(2);
     if (wave_id() == 0) finalize_heads<G>(sm.u.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
     __syncthreads();
@@ -250,7 +250,7 @@ __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_search(NetParams np, SearchParams sp, EngineArrays E,
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_search(NetParams np, SearchParams sp, EngineArrays E,
                                                       const float* __restrict__ root_obs,
                                                       const double* __restrict__ noise, int game_base,
                                                       int move_index, int* out_visits, double* out_value) {
@@ -303,7 +303,7 @@ __device__ __forceinline__ float board_plane(const Smem<G>& sm, const BoardMeta&
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_board_reset(EngineArrays E) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_board_reset(EngineArrays E) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
   for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(kThreads) k_board_reset(EngineArrays E) {
 // Step every slot with actions[g] >= 0 (gogame.next_state); status[g] gets a
 // BOARD_* code; winner[g] = GoEnv.winner() after the step (0 unless ended).
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_board_step(EngineArrays E, const int* __restrict__ actions,
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_board_step(EngineArrays E, const int* __restrict__ actions,
                                                           int* status, double* winner, double komi) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(kThreads) k_board_step(EngineArrays E, const i
 
 // f64 observation planes [G][6][CELLS] of the current boards (GoEnv state)
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_board_planes(EngineArrays E, double* planes) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_board_planes(EngineArrays E, double* planes) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
   const int* mm = E.meta + g * 4;
@@ -468,7 +468,7 @@ struct PlayParams {
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
                                                              EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Diagnostic variant of libmzgo.so with per-phase s_memtime stamps
-# (-DMZGO_STAMPS).  Load it with MZGO_LIB=muzero-go_amd/mzgo/libmzgo_stamps.so.
+# (-DMZGO_STAMPS).  Load it with MZGO_LIB=muzero-go_amd/mzgo/libmzgo_${VARIANT:-stamps}.so.
 set -e
 cd "$(dirname "$0")/.."
-B=muzero-go_amd/build_stamps
+B=muzero-go_amd/build_${VARIANT:-stamps}
 mkdir -p $B
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result -DMZGO_STAMPS"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result -DMZGO_STAMPS $EXTRA"
 for f in muzero-go_amd/csrc/*.hip; do /opt/rocm/bin/hipcc $FLAGS -c -o $B/$(basename ${f%.hip}).o $f & done
 wait
-/opt/rocm/bin/hipcc $FLAGS -shared -o muzero-go_amd/mzgo/libmzgo_stamps.so $B/*.o
+/opt/rocm/bin/hipcc $FLAGS -shared -o muzero-go_amd/mzgo/libmzgo_${VARIANT:-stamps}.so $B/*.o

@@ -79,12 +79,12 @@ def stamps_report():
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
     ms = timeit(lambda: seng.search(obs), reps=1)
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))
-    names = ["select", "stage", "conv", "heads", "priors", "backup", "-", "-"]
+    names = ["select", "stage", "conv_epilogue", "heads", "priors", "backup", "conv_loop", "conv_sync"]
     per_sim = buf.astype(np.float64).mean(0) / (2 * S)            # warm-up call inside timeit + 1 rep
-    total = per_sim[:6].sum()
+    total = per_sim.sum()
     print(json.dumps({"N": N, "G": G, "S": S, "search_ms": ms,
-                      "cycles_per_sim": {n: round(float(v)) for n, v in zip(names, per_sim) if n != "-"},
-                      "share": {n: round(float(v / total), 3) for n, v in zip(names, per_sim) if n != "-"},
+                      "cycles_per_sim": {n: round(float(v)) for n, v in zip(names, per_sim) },
+                      "share": {n: round(float(v / total), 3) for n, v in zip(names, per_sim)},
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 
