@@ -9,7 +9,8 @@ select / dynamics+prediction (MFMA) / expand / backup, action choice, board
 step).  Games restart (new epoch) every max_moves steps, so any --steps works.
 
 Multi-GPU (torchrun, one process per GPU): games are sharded by global id
-(rank * G + slot); no collective in the data path (scaling "weak").
+(rank * G + slot); the only collective is the end-of-run RCCL gather of every
+rank's game records to rank 0 (inside the timed region); scaling "weak".
 
 Prints ONE JSON line on rank 0.
 """
@@ -135,6 +136,11 @@ def main():
         sp.move()
         ev[i][1].record(stream)
         step_no += 1
+    if world > 1:
+        # the trajectory gather of config 3: every rank's packed game records
+        # to rank 0's HBM over RCCL (the only collective on the data path)
+        from mzgo import distributed as mdist
+        mdist.gather_packed(mdist.pack_engine(eng), to_host=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -146,6 +146,15 @@ int mzgo_records_export(mzgo_engine* eng, int g, int32_t* length_host, int32_t* 
                         int32_t* action_host, double* value_host, double* policy_host,
                         double* reward_host, double* final_reward_host, void* stream);
 
+/* All slots' records packed into one DEVICE buffer (the multi-GPU trajectory
+ * gather moves it with RCCL).  dst NULL: only report *bytes_needed.  Layout,
+ * each field padded to 16 bytes, G slots, M = max_moves, C = N*N, A = C+1:
+ *   stones i8 [G][M][C] | invd u8 [G][M][C] | flags u8 [G][M] | action i32 [G][M] |
+ *   value f64 [G][M] | policy f64 [G][M][A] | reward f64 [G][M] |
+ *   meta i32 [G][4] (turn, passed, done, length) | status i32 [G] | final_reward f64 [G] */
+int mzgo_records_pack(mzgo_engine* eng, uint8_t* dst, int64_t capacity, int64_t* bytes_needed,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -483,4 +483,25 @@ int mzgo_debug_stamps(mzgo_engine* e, unsigned long long* host) {
 }
 #endif
 
+// Packed records of all G slots, for the multi-GPU gather (layout in mzgo.h).
+int mzgo_records_pack(mzgo_engine* e, uint8_t* dst, int64_t capacity, int64_t* bytes_needed, void* stream) {
+  if (!e || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  const size_t G = e->G, M = e->M, CELLS = e->CELLS, A = e->A;
+  const size_t sizes[] = {G * M * CELLS, G * M * CELLS, G * M, G * M * 4, G * M * 8, G * M * A * 8,
+                          G * M * 8, G * 4 * 4, G * 4, G * 8};
+  const void* srcs[] = {e->E.rec_stones, e->E.rec_invd, e->E.rec_flags, e->E.rec_action, e->E.rec_value,
+                        e->E.rec_policy, e->E.rec_reward, e->E.meta, e->E.status, e->E.final_reward};
+  size_t total = 0;
+  for (size_t s : sizes) total += (s + 15) / 16 * 16;
+  if (bytes_needed) *bytes_needed = (int64_t)total;
+  if (!dst) return MZGO_OK;
+  if (capacity < (int64_t)total) return fail(MZGO_EINVAL, "records_pack: buffer of %lld bytes, need %zu", (long long)capacity, total);
+  size_t off = 0;
+  for (int i = 0; i < 10; ++i) {
+    HIPCHK(hipMemcpyAsync(dst + off, srcs[i], sizes[i], hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    off += (sizes[i] + 15) / 16 * 16;
+  }
+  return MZGO_OK;
+}
+
 }  // extern "C"

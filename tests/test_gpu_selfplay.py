@@ -95,3 +95,21 @@ def test_records_pickle_roundtrip(tmp_path):
     assert len(batch) == 2                      # games 2..3 (the reference's slice)
     assert set(batch[0]) == {"observations", "actions", "policies", "values", "rewards", "returns",
                              "final_reward"}
+
+
+def test_records_pack_matches_export():
+    """mzgo_records_pack (what the multi-GPU gather moves) == per-slot export."""
+    import mzgo
+    from mzgo import distributed as mdist
+    sp = mzgo.SelfPlay(_net(5), 4, 6, seed=21)
+    sp.reset()
+    for _ in range(9):
+        sp.move()
+    buf = mdist.pack_engine(sp.engine).cpu().numpy()
+    arrays = mdist.unpack(buf, sp.engine.G, sp.engine.M, 5)
+    for g in range(4):
+        want = sp.engine.record(g)
+        got = mdist.slot_records(arrays, g)
+        assert got["length"] == want["length"] == 9
+        for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
+            np.testing.assert_array_equal(got[k], want[k], err_msg=k)
