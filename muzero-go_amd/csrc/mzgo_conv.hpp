@@ -52,7 +52,15 @@ __device__ __forceinline__ void stage_board(float* __restrict__ lds, const float
     for (int i = threadIdx.x; i < nch * Q; i += kThreads) {
       int c = i / Q, q = i - c * Q;
       float4 v = s4[c * Q + q];
-      if (emb) { float e = emb[c]; v.x += e; v.y += e; v.z += e; v.w += e; }
+      if (emb) {
+        const float e = emb[c];
+        // cells >= N*N are pad: keep them 0 (the zero slot of conv3x3_ring)
+        const int j0 = q * 4;
+        v.x = j0 + 0 < G::CELLS ? v.x + e : 0.f;
+        v.y = j0 + 1 < G::CELLS ? v.y + e : 0.f;
+        v.z = j0 + 2 < G::CELLS ? v.z + e : 0.f;
+        v.w = j0 + 3 < G::CELLS ? v.w + e : 0.f;
+      }
       *reinterpret_cast<float4*>(lds + c * G::CPAD + q * 4) = v;
     }
   } else {
@@ -62,8 +70,17 @@ __device__ __forceinline__ void stage_board(float* __restrict__ lds, const float
       if (emb) v += emb[c];
       lds[c * G::CPAD + j] = v;
     }
+    for (int c = threadIdx.x; c < nch; c += kThreads) lds[c * G::CPAD + G::CELLS] = 0.f;
   }
 }
+
+// Cell N*N of every staged LDS row is 0 (the "zero slot"): invalid taps of
+// conv3x3_ring read it instead of being masked with v_cndmask.  Pooled
+// latents (stride CS) keep 0 in their pad cells, so the 16-byte staging copy
+// carries it (and the emb add skips pad cells); the scalar path writes it.
+static_assert(Geo<9, 96>::CELLS < Geo<9, 96>::CS && Geo<19, 96>::CELLS < Geo<19, 96>::CS &&
+              Geo<5, 96>::CELLS < Geo<5, 96>::CS && Geo<6, 96>::CELLS < Geo<6, 96>::CS,
+              "every supported board has a pad cell to serve as the zero slot");
 
 // Zero channels [c0, c1) of an LDS board (input padding of conv1: 6 -> 8 ch).
 template <class G>
@@ -188,6 +205,7 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
           float v = acc[mi][ni][r] + bb;
           v = v > 0.f ? v : 0.f;
           const int cell = (cg * NG + ni) * 16 + col;
+          v = cell < G::CELLS ? v : 0.f;                    // pad cells stay 0 (zero slot)
           if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
 #pragma unroll
           for (int h = 0; h < NH; ++h) hsum[h][ni] = __builtin_fmaf(hw[h], v, hsum[h][ni]);
@@ -343,7 +361,6 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
     for (int c = 0; c < NSLOT - 1; ++c)
       if (c < NCH) issue(c);
     int off[JW][NG];
-    bool ok[JW][NG];
     for (int c = 0; c < NCH; ++c) {
       if (c + NSLOT - 1 < NCH) {
         issue(c + NSLOT - 1);
@@ -361,8 +378,8 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
 #pragma unroll
           for (int ni = 0; ni < NG; ++ni) {
             const int yy = cy[j][ni] + dy, xx = cx[j][ni] + dx;
-            ok[j][ni] = live[j][ni] && yy >= 0 && yy < G::N && xx >= 0 && xx < G::N;
-            off[j][ni] = ok[j][ni] ? yy * G::N + xx : 0;
+            const bool ok = live[j][ni] && yy >= 0 && yy < G::N && xx >= 0 && xx < G::N;
+            off[j][ni] = ok ? yy * G::N + xx : G::CELLS;      // zero slot
           }
       }
       const float* slot = myring + (c % NSLOT) * (R::SLOT / 4) + lane * MGP;
@@ -382,7 +399,7 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
 #pragma unroll
         for (int j = 0; j < JW; ++j)
 #pragma unroll
-          for (int ni = 0; ni < NG; ++ni) b[j][ni] = ok[j][ni] ? b_nx[j][ni] : 0.f;
+          for (int ni = 0; ni < NG; ++ni) b[j][ni] = b_nx[j][ni];
         if (kk + 1 < KC) {
           a_nx = lds_frag<MGP>(slot + (kk + 1) * 64 * MGP);
 #pragma unroll
@@ -432,6 +449,7 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
             float v = acc[j][mi][ni][r] + bb;
             v = v > 0.f ? v : 0.f;
             const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
+            v = cell < G::CELLS ? v : 0.f;                  // pad cells stay 0 (zero slot)
             if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
 #pragma unroll
             for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h], v, hsum[h][j][ni]);

@@ -110,15 +110,16 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
   zero_channels<G>(sm.u.in, 6, 8);
   __syncthreads();
   HeadPart<G> hp{sm.u.hp};
-  conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, G::CELLS, nullptr, hp);
+  const int oc = lat_stride == G::CS ? G::CS : G::CELLS;   // pooled latents also write their 0 pads
+  conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
   __syncthreads();
   stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
   __syncthreads();
-  conv3x3_ring<G, 64, 64, 0>(sm.u.in, sm.ring, np.w_conv2, np.b_conv2, lat, lat_stride, G::CELLS,
+  conv3x3_ring<G, 64, 64, 0>(sm.u.in, sm.ring, np.w_conv2, np.b_conv2, lat, lat_stride, oc,
                              nullptr, sm.u.hp);
   stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
   __syncthreads();
-  conv3x3_ring<G, 64, G::C, 2>(sm.u.in, sm.ring, np.w_conv3, np.b_conv3, lat, lat_stride, G::CELLS,
+  conv3x3_ring<G, 64, G::C, 2>(sm.u.in, sm.ring, np.w_conv3, np.b_conv3, lat, lat_stride, oc,
                                np.head_w + G::C, sm.u.hp);
   if (wave_id() == 0) finalize_heads<G>(sm.u.hp, false, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
   __syncthreads();
