@@ -52,11 +52,11 @@ __device__ __forceinline__ bool nbr(int c, int d, int& n) {
 // class(c) is equal; -1 where class(c) == 0.
 template <class G, class ClassFn>
 __device__ __forceinline__ void label_components(int* label, ClassFn cls) {
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) label[c] = cls(c) ? c : -1;
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) label[c] = cls(c) ? c : -1;
   __syncthreads();
   for (int it = 0; it < G::CELLS + 2; ++it) {
     int changed = 0;
-    for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+    for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
       const int k = cls(c);
       if (!k) continue;
       int m = label[c];
@@ -76,9 +76,9 @@ __device__ __forceinline__ void label_components(int* label, ClassFn cls) {
 // libs[g] = #distinct empty points adjacent to group g; gsize[g] = #stones
 template <class G>
 __device__ __forceinline__ void count_liberties(BoardLds<G>& b, bool sizes) {
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) { b.libs[c] = 0; if (sizes) b.gsize[c] = 0; }
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) { b.libs[c] = 0; if (sizes) b.gsize[c] = 0; }
   __syncthreads();
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     if (b.stone[c]) {
       if (sizes) atomicAdd(&b.gsize[b.label[c]], 1);
       continue;
@@ -102,7 +102,7 @@ __device__ __forceinline__ void count_liberties(BoardLds<G>& b, bool sizes) {
 // INVD plane for the opponent of ``mover`` (state_utils.compute_invalid_moves)
 template <class G>
 __device__ __forceinline__ void compute_invalid(BoardLds<G>& b, int mover, int ko) {
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     uint8_t inv;
     if (b.stone[c]) {
       inv = 1;
@@ -175,7 +175,7 @@ __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int acti
     const int nk = b.misc[0];
     ko = b.misc[2];
     if (nk > 0) {
-      for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+      for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
         if (b.stone[c] == 2 - player) {
           const int l = b.label[c];
           bool dead = false;
@@ -197,9 +197,9 @@ __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int acti
 template <class G>
 __device__ __forceinline__ double board_winning(BoardLds<G>& b, double komi) {
   label_components<G>(b.label, [&](int c) { return b.stone[c] == 0 ? 1 : 0; });
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) { b.libs[c] = 0; b.gsize[c] = 0; }
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) { b.libs[c] = 0; b.gsize[c] = 0; }
   __syncthreads();
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     if (b.stone[c]) continue;
     int f = 0;
 #pragma unroll
@@ -212,7 +212,7 @@ __device__ __forceinline__ double board_winning(BoardLds<G>& b, double komi) {
   }
   __syncthreads();
   int black = 0, white = 0;
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     if (b.stone[c] == 1) black++;
     else if (b.stone[c] == 2) white++;
     else if (b.label[c] == c) {

@@ -72,12 +72,13 @@ std::vector<Spec> specs(int C, int A) {
 // conv weight W[cout][cin][3][3] -> MFMA A-fragment order of mzgo_conv.hpp:
 // packed[((s * NCOG + cog) * 64 + lane) * MGP + mi] with k-step s = tap*CQ + c4,
 // cout = (cog*MG + mi)*16 + (lane & 15), cin = c4*4 + (lane >> 4).
-// With cog_major the layout is packed[((cog * KS + s) * 64 + lane) * MGP + mi]
-// (one contiguous stream per cout group, for the per-wave DMA rings of
-// conv3x3_ring); otherwise [((s * NCOG + cog) * 64 + lane) * MGP + mi]
+// With cog_major the layout is packed[(frag * 64 + lane) * MGP + mi] with
+// frag = ((cog * ksplit + half) * 9 + tap) * (CQ / ksplit) + c4 % (CQ / ksplit):
+// one contiguous stream per (cout group, k-half) for the per-wave DMA rings
+// of conv3x3_ring (ksplit = Geo::KSPLIT); otherwise frag = s * NCOG + cog
 // (conv3x3_direct).
-std::vector<float> pack_conv(const float* W, int COUT, int CIN, bool cog_major) {
-  const int CINP = (CIN + 3) / 4 * 4, CQ = CINP / 4, KS = 9 * CQ;
+std::vector<float> pack_conv(const float* W, int COUT, int CIN, bool cog_major, int ksplit = 1) {
+  const int CINP = (CIN + 3) / 4 * 4, CQ = CINP / 4, KS = 9 * CQ, CQH = CQ / ksplit;
   const int MT = COUT / 16;
   const int MG = (MT % 3 == 0) ? 3 : ((MT % 4 == 0 && MT >= 8) ? 4 : 2);
   const int MGP = MG == 3 ? 4 : MG, NCOG = MT / MG;
@@ -90,7 +91,10 @@ std::vector<float> pack_conv(const float* W, int COUT, int CIN, bool cog_major) 
           const int cout = (cog * MG + mi) * 16 + (lane & 15);
           const int cin = c4 * 4 + (lane >> 4);
           const float v = cin < CIN ? W[(((size_t)cout * CIN + cin) * 3 + ky) * 3 + kx] : 0.f;
-          const size_t frag = cog_major ? (size_t)cog * KS + s : (size_t)s * NCOG + cog;
+          // cog-major streams are further ordered [half][tap][c4 within the half]
+          const int half = c4 / CQH, c4h = c4 % CQH;
+          const size_t frag = cog_major ? (((size_t)cog * ksplit + half) * 9 + t) * CQH + c4h
+                                        : (size_t)s * NCOG + cog;
           out[(frag * 64 + lane) * MGP + mi] = v;
         }
   }
@@ -140,11 +144,14 @@ struct mzgo_engine {
     std::vector<std::vector<float>> parts;
     parts.push_back(pack_conv(sd["representation.conv1.weight"].data(), 64, 6, false));
     parts.push_back(sd["representation.conv1.bias"]);
-    parts.push_back(pack_conv(sd["representation.conv2.weight"].data(), 64, 64, true));
+    // k-range split of the ring conv: 2 when the board runs 8 waves (Geo::KSPLIT)
+    const int ct = (N * N + 15) / 16, ng = ct >= 3 ? 3 : ct, ncg = (ct + ng - 1) / ng;
+    const int ksplit = ncg <= 2 ? 2 : 1;
+    parts.push_back(pack_conv(sd["representation.conv2.weight"].data(), 64, 64, true, ksplit));
     parts.push_back(sd["representation.conv2.bias"]);
-    parts.push_back(pack_conv(sd["representation.conv3.weight"].data(), C, 64, true));
+    parts.push_back(pack_conv(sd["representation.conv3.weight"].data(), C, 64, true, ksplit));
     parts.push_back(sd["representation.conv3.bias"]);
-    parts.push_back(pack_conv(sd["dynamics.conv.weight"].data(), C, C, true));
+    parts.push_back(pack_conv(sd["dynamics.conv.weight"].data(), C, C, true, ksplit));
     parts.push_back(sd["dynamics.conv.bias"]);
     parts.push_back(sd["dynamics.action_embedding.weight"]);
     std::vector<float> hw;

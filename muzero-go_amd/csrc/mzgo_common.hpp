@@ -10,8 +10,9 @@
 
 namespace mzgo {
 
-constexpr int kThreads = 256;  // 4 waves of 64 per workgroup, one workgroup per game
-constexpr int kWaves = kThreads / 64;
+// One workgroup per game.  Boards with one cell job per cout group (5x5, 6x6,
+// 9x9) run 8 waves = 2 per SIMD, the wave pairs splitting the conv k-range;
+// 19x19 runs 4 waves (its 4 cell jobs per wave need every register).
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -32,6 +33,9 @@ struct Geo {
   static constexpr int NG = CT >= 3 ? 3 : CT;     // cell tiles per wave job
   static constexpr int NCG = (CT + NG - 1) / NG;  // cell groups
   static constexpr int AP = (A + 63) / 64;        // actions per lane (a = lane + 64*j)
+  static constexpr int WAVES = NCG <= 2 ? 8 : 4;  // waves per workgroup
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int KSPLIT = WAVES / 4;        // conv k-range split over wave halves
   static_assert(C % 16 == 0, "latent_dim must be a multiple of 16");
 };
 

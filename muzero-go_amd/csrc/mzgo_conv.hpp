@@ -49,7 +49,7 @@ __device__ __forceinline__ void stage_board(float* __restrict__ lds, const float
   if (src_stride == G::CS) {
     constexpr int Q = G::CS / 4;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (int i = threadIdx.x; i < nch * Q; i += kThreads) {
+    for (int i = threadIdx.x; i < nch * Q; i += G::THREADS) {
       int c = i / Q, q = i - c * Q;
       float4 v = s4[c * Q + q];
       if (emb) {
@@ -64,13 +64,13 @@ __device__ __forceinline__ void stage_board(float* __restrict__ lds, const float
       *reinterpret_cast<float4*>(lds + c * G::CPAD + q * 4) = v;
     }
   } else {
-    for (int i = threadIdx.x; i < nch * G::CELLS; i += kThreads) {
+    for (int i = threadIdx.x; i < nch * G::CELLS; i += G::THREADS) {
       int c = i / G::CELLS, j = i - c * G::CELLS;
       float v = src[c * src_stride + j];
       if (emb) v += emb[c];
       lds[c * G::CPAD + j] = v;
     }
-    for (int c = threadIdx.x; c < nch; c += kThreads) lds[c * G::CPAD + G::CELLS] = 0.f;
+    for (int c = threadIdx.x; c < nch; c += G::THREADS) lds[c * G::CPAD + G::CELLS] = 0.f;
   }
 }
 
@@ -85,7 +85,7 @@ static_assert(Geo<9, 96>::CELLS < Geo<9, 96>::CS && Geo<19, 96>::CELLS < Geo<19,
 // Zero channels [c0, c1) of an LDS board (input padding of conv1: 6 -> 8 ch).
 template <class G>
 __device__ __forceinline__ void zero_channels(float* lds, int c0, int c1) {
-  for (int i = threadIdx.x; i < (c1 - c0) * G::CPAD; i += kThreads) lds[c0 * G::CPAD + i] = 0.f;
+  for (int i = threadIdx.x; i < (c1 - c0) * G::CPAD; i += G::THREADS) lds[c0 * G::CPAD + i] = 0.f;
 }
 
 // Head accumulation target: hp[cog][h][cell] in LDS, summed in fixed order later.
@@ -122,7 +122,7 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
   const int kq = lane >> 4;       // k row of this lane inside a k-step (B operand)
   const int col = lane & 15;      // cell column of this lane (B operand / accumulator)
 
-  for (int job = wave; job < JOBS; job += kWaves) {
+  for (int job = wave; job < JOBS; job += G::WAVES) {
     const int cog = job % S::NCOG;
     const int cg = job / S::NCOG;
 
@@ -245,13 +245,14 @@ template <class G, int COUT>
 struct Ring {
   typedef ConvShape<COUT> S;
   static constexpr int KSTEP_BYTES = 64 * S::MGP * 4;       // one cog, one k-step (1 KiB or 512 B)
-  static constexpr int JPW = kWaves / S::NCOG;              // waves sharing one cout group
+  static constexpr int JPW = 4 / S::NCOG;                   // waves of one k-half sharing a cout group
   static constexpr int JW = (G::NCG + JPW - 1) / JPW;       // cell-group jobs per wave
-  static constexpr int KC = JW >= 2 ? (1024 / KSTEP_BYTES) : 8;   // k-steps per chunk
+  static constexpr int KC = JW >= 2 ? (1024 / KSTEP_BYTES)  // k-steps per chunk
+                                    : (G::KSPLIT == 2 ? 4096 / KSTEP_BYTES : 8);
   static constexpr int NSLOT = JW >= 2 ? 2 : 3;
   static constexpr int SLOT = KC * KSTEP_BYTES;             // bytes per slot (multiple of 1 KiB)
   static constexpr int NGLDS = SLOT / 1024;                 // DMA instructions per chunk
-  static_assert(kWaves % S::NCOG == 0, "waves must split evenly over cout groups");
+  static_assert(4 % S::NCOG == 0, "a k-half's 4 waves must split evenly over cout groups");
   static_assert(SLOT % 1024 == 0, "slots are whole 1-KiB DMA pieces");
 };
 
@@ -259,7 +260,7 @@ template <class G>
 struct RingBytes {
   static constexpr int a = Ring<G, 64>::NSLOT * Ring<G, 64>::SLOT;
   static constexpr int b = Ring<G, G::C>::NSLOT * Ring<G, G::C>::SLOT;
-  static constexpr int value = kWaves * (a > b ? a : b);   // all waves' private rings
+  static constexpr int value = G::WAVES * (a > b ? a : b);  // all waves' private rings
 };
 
 // 16 bytes per lane global -> LDS (global_load_lds_dwordx4).  Issued from
@@ -306,21 +307,25 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
   typedef Ring<G, COUT> R;
   constexpr int CINP = (CIN + 3) / 4 * 4;
   constexpr int CQ = CINP / 4;
-  constexpr int KS = 9 * CQ;
-  constexpr int KC = R::KC, NCH = KS / KC, JW = R::JW, NG = G::NG, MG = S::MG, MGP = S::MGP;
+  constexpr int KSPLIT = G::KSPLIT;
+  constexpr int CQH = CQ / KSPLIT;                // channel quads of one k-half per tap
+  constexpr int KSH = 9 * CQH;                    // k-steps per wave
+  constexpr int KC = R::KC, NCH = KSH / KC, JW = R::JW, NG = G::NG, MG = S::MG, MGP = S::MGP;
   constexpr int NSLOT = R::NSLOT;
-  static_assert(CQ % KC == 0, "a chunk must not straddle two taps");
+  static_assert(CQ % KSPLIT == 0 && CQH % KC == 0, "a chunk must not straddle two taps");
   static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
   typedef typename WFrag<MGP>::T wfrag;
 
   const int lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());   // scalar: uniform branches
+  const int half = wave / 4, wl = wave % 4;                      // k-half, wave within the half
   const int kq = lane >> 4, col = lane & 15;
-  const int cog = wave % S::NCOG;
-  const int cg0 = wave / S::NCOG;
-  // this wave's contiguous weight stream and private ring
-  const char* wsrc = reinterpret_cast<const char*>(wpk) + (size_t)cog * KS * R::KSTEP_BYTES + lane * 16;
-  float* myring = ring + wave * (RingBytes<G>::value / kWaves / 4);
+  const int cog = wl % S::NCOG;
+  const int cg0 = wl / S::NCOG;
+  // this wave's contiguous weight stream ([cog][half][tap][c4'] order) and private ring
+  const char* wsrc = reinterpret_cast<const char*>(wpk) + (size_t)(cog * KSPLIT + half) * KSH * R::KSTEP_BYTES +
+                     lane * 16;
+  float* myring = ring + wave * (RingBytes<G>::value / G::WAVES / 4);
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_addr(myring));
 
   // every job of every wave covers a real cell group unless NCG % JPW != 0
@@ -369,9 +374,10 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
         wait_vmcnt<0>();
       }
       const int s0 = c * KC;
-      const int t = s0 / CQ;
-      const int c40 = s0 - t * CQ;
-      if (c40 == 0) {
+      const int t = s0 / CQH;
+      const int c4h = s0 - t * CQH;
+      const int c40 = half * CQH + c4h;           // channel quad of this chunk's first k-step
+      if (c4h == 0) {
         const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
 #pragma unroll
         for (int j = 0; j < JW; ++j)
@@ -420,7 +426,34 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
     }
   }
   if (st) st->lap(6);
-  __syncthreads();   // every wave is done with lds_in
+  __syncthreads();   // every wave is done with lds_in and its ring
+  if constexpr (KSPLIT == 2) {
+    // second k-half hands its partial accumulators to its partner through the
+    // (now idle) rings; the first half adds them in a fixed order
+    float* red = ring + wl * (JW * MG * NG * 4 * 64);
+    static_assert(4 * JW * MG * NG * 4 * 64 * 4 <= RingBytes<G>::value, "reduction fits the rings");
+    if (half == 1 && active) {
+#pragma unroll
+      for (int j = 0; j < JW; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MG; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NG; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[(((j * MG + mi) * NG + ni) * 4 + r) * 64 + lane] = acc[j][mi][ni][r];
+    }
+    __syncthreads();
+    if (half == 0 && active) {
+#pragma unroll
+      for (int j = 0; j < JW; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MG; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NG; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[j][mi][ni][r] += red[(((j * MG + mi) * NG + ni) * 4 + r) * 64 + lane];
+    }
+  }
   if (st) st->lap(7);
 
   // ---- epilogue: bias + ReLU, store, fused 1x1 heads ----
@@ -431,7 +464,7 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
     for (int j = 0; j < JW; ++j)
 #pragma unroll
       for (int ni = 0; ni < NG; ++ni) hsum[h][j][ni] = 0.f;
-  if (active) {
+  if (active && half == 0) {
 #pragma unroll
     for (int mi = 0; mi < MG; ++mi) {
       const int cout0 = (cog * MG + mi) * 16 + kq * 4;

@@ -30,38 +30,38 @@ template <int N, int C>
 struct Launch {
   static hipError_t ii(const NetParams& np, const float* obs, int B, float* lat, float* val,
                        float* logits, hipStream_t s) {
-    hipLaunchKernelGGL((k_initial_inference<N, C>), dim3(B), dim3(kThreads), 0, s, np, obs, lat, val, logits);
+    hipLaunchKernelGGL((k_initial_inference<N, C>), dim3(B), dim3(Geo<N, C>::THREADS), 0, s, np, obs, lat, val, logits);
     return hipGetLastError();
   }
   static hipError_t ri(const NetParams& np, const float* lat, const int64_t* act, int B, float* nlat,
                        float* rew, float* val, float* logits, int* err, hipStream_t s) {
-    hipLaunchKernelGGL((k_recurrent_inference<N, C>), dim3(B), dim3(kThreads), 0, s, np, lat, act, nlat,
+    hipLaunchKernelGGL((k_recurrent_inference<N, C>), dim3(B), dim3(Geo<N, C>::THREADS), 0, s, np, lat, act, nlat,
                        rew, val, logits, err);
     return hipGetLastError();
   }
   static hipError_t search(const NetParams& np, const SearchParams& sp, const EngineArrays& E,
                            const float* obs, const double* noise, int G, int game_base, int move,
                            int* visits, double* value, hipStream_t s) {
-    hipLaunchKernelGGL((k_search<N, C>), dim3(G), dim3(kThreads), 0, s, np, sp, E, obs, noise, game_base,
+    hipLaunchKernelGGL((k_search<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, np, sp, E, obs, noise, game_base,
                        move, visits, value);
     return hipGetLastError();
   }
   static hipError_t breset(const EngineArrays& E, int G, hipStream_t s) {
-    hipLaunchKernelGGL((k_board_reset<N, C>), dim3(G), dim3(kThreads), 0, s, E);
+    hipLaunchKernelGGL((k_board_reset<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, E);
     return hipGetLastError();
   }
   static hipError_t bstep(const EngineArrays& E, int G, const int* act, int* status, double* winner,
                           double komi, hipStream_t s) {
-    hipLaunchKernelGGL((k_board_step<N, C>), dim3(G), dim3(kThreads), 0, s, E, act, status, winner, komi);
+    hipLaunchKernelGGL((k_board_step<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, E, act, status, winner, komi);
     return hipGetLastError();
   }
   static hipError_t bplanes(const EngineArrays& E, int G, double* planes, hipStream_t s) {
-    hipLaunchKernelGGL((k_board_planes<N, C>), dim3(G), dim3(kThreads), 0, s, E, planes);
+    hipLaunchKernelGGL((k_board_planes<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, E, planes);
     return hipGetLastError();
   }
   static hipError_t move(const NetParams& np, const SearchParams& sp, const PlayParams& pp,
                          const EngineArrays& E, int G, hipStream_t s) {
-    hipLaunchKernelGGL((k_selfplay_move<N, C>), dim3(G), dim3(kThreads), 0, s, np, sp, pp, E);
+    hipLaunchKernelGGL((k_selfplay_move<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, np, sp, pp, E);
     return hipGetLastError();
   }
   static KernelSet table() {

@@ -103,7 +103,7 @@ __device__ __forceinline__ BoardLds<G> board_lds(Smem<G>& sm) {
 template <class G, class PlaneFn>
 __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
                                       int lat_stride) {
-  for (int i = threadIdx.x; i < 6 * G::CELLS; i += kThreads) {
+  for (int i = threadIdx.x; i < 6 * G::CELLS; i += G::THREADS) {
     const int c = i / G::CELLS, j = i - c * G::CELLS;
     sm.u.in[c * G::CPAD + j] = planes(c, j);
   }
@@ -142,7 +142,7 @@ __device__ __forceinline__ void dynamics(Smem<G>& sm, const NetParams& np, const
 // Batched drop-in inference (self_play.py:121-128)
 // ---------------------------------------------------------------------------
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_initial_inference(NetParams np, const float* __restrict__ obs,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_initial_inference(NetParams np, const float* __restrict__ obs,
                                                                  float* latent, float* value, float* logits) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -150,12 +150,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
   const float* o = obs + (size_t)b * 6 * G::CELLS;
   float* lat = latent + (size_t)b * G::C * G::CELLS;
   representation<G>(sm, np, [&](int c, int j) { return o[c * G::CELLS + j]; }, lat, G::CELLS);
-  for (int a = threadIdx.x; a < G::A; a += kThreads) logits[(size_t)b * G::A + a] = sm.t.logits[a];
+  for (int a = threadIdx.x; a < G::A; a += G::THREADS) logits[(size_t)b * G::A + a] = sm.t.logits[a];
   if (threadIdx.x == 0) value[b] = sm.t.value;
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
                                                                    const int64_t* __restrict__ action,
                                                                    float* next_latent, float* reward,
                                                                    float* value, float* logits, int* err) {
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
   }
   dynamics<G>(sm, np, latent + (size_t)b * G::C * G::CELLS, G::CELLS, (int)a,
               next_latent + (size_t)b * G::C * G::CELLS, G::CELLS);
-  for (int i = threadIdx.x; i < G::A; i += kThreads) logits[(size_t)b * G::A + i] = sm.t.logits[i];
+  for (int i = threadIdx.x; i < G::A; i += G::THREADS) logits[(size_t)b * G::A + i] = sm.t.logits[i];
   if (threadIdx.x == 0) { reward[b] = sm.t.reward; value[b] = sm.t.value; }
 }
 
@@ -208,7 +208,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
     }
     const int nid = nodes++;
     int* crow = T.child + (size_t)nid * G::A;
-    for (int i = threadIdx.x; i < G::A; i += kThreads) crow[i] = -1;
+    for (int i = threadIdx.x; i < G::A; i += G::THREADS) crow[i] = -1;
     if (threadIdx.x == 0) { T.visits[nid] = 0; T.wsum[nid] = 0.0; }
     stage_board<G>(sm.u.in, pool + (size_t)leaf * node_floats, G::CS, G::C, np.emb + (size_t)a * G::C);
     __syncthreads();
@@ -240,7 +240,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
 template <class G>
 __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int* out_visits, double* out_value) {
   const TreeView T = TreeViewOf<G>::make(E, g);
-  for (int a = threadIdx.x; a < G::A; a += kThreads) {
+  for (int a = threadIdx.x; a < G::A; a += G::THREADS) {
     const int c = T.child[a];
     if (out_visits) out_visits[(size_t)g * G::A + a] = c >= 0 ? T.visits[c] : 0;
   }
@@ -251,7 +251,7 @@ __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_search(NetParams np, SearchParams sp, EngineArrays E,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_search(NetParams np, SearchParams sp, EngineArrays E,
                                                       const float* __restrict__ root_obs,
                                                       const double* __restrict__ noise, int game_base,
                                                       int move_index, int* out_visits, double* out_value) {
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
 // ---------------------------------------------------------------------------
 template <class G>
 __device__ __forceinline__ void load_board(Smem<G>& sm, const EngineArrays& E, int g, BoardMeta& m) {
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     sm.stone[c] = E.stones[(size_t)g * G::CELLS + c];
     sm.invd[c] = E.invd[(size_t)g * G::CELLS + c];
   }
@@ -281,7 +281,7 @@ __device__ __forceinline__ void load_board(Smem<G>& sm, const EngineArrays& E, i
 
 template <class G>
 __device__ __forceinline__ void store_board(Smem<G>& sm, const EngineArrays& E, int g, const BoardMeta& m) {
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     E.stones[(size_t)g * G::CELLS + c] = sm.stone[c];
     E.invd[(size_t)g * G::CELLS + c] = sm.invd[c];
   }
@@ -304,10 +304,10 @@ __device__ __forceinline__ float board_plane(const Smem<G>& sm, const BoardMeta&
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_board_reset(EngineArrays E) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_board_reset(EngineArrays E) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     E.stones[(size_t)g * G::CELLS + c] = 0;
     E.invd[(size_t)g * G::CELLS + c] = 0;
   }
@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
 // Step every slot with actions[g] >= 0 (gogame.next_state); status[g] gets a
 // BOARD_* code; winner[g] = GoEnv.winner() after the step (0 unless ended).
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_board_step(EngineArrays E, const int* __restrict__ actions,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_board_step(EngineArrays E, const int* __restrict__ actions,
                                                           int* status, double* winner, double komi) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -341,12 +341,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
 
 // f64 observation planes [G][6][CELLS] of the current boards (GoEnv state)
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_board_planes(EngineArrays E, double* planes) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_board_planes(EngineArrays E, double* planes) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
   const int* mm = E.meta + g * 4;
   double* p = planes + (size_t)g * 6 * G::CELLS;
-  for (int j = threadIdx.x; j < G::CELLS; j += kThreads) {
+  for (int j = threadIdx.x; j < G::CELLS; j += G::THREADS) {
     const int s = E.stones[(size_t)g * G::CELLS + j];
     p[j] = s == 1; p[G::CELLS + j] = s == 2; p[2 * G::CELLS + j] = mm[0];
     p[3 * G::CELLS + j] = E.invd[(size_t)g * G::CELLS + j];
@@ -469,7 +469,7 @@ struct PlayParams {
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
                                                              EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -479,7 +479,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1
   load_board<G>(sm, E, g, m);
   const int mv = m.moves;
   const size_t rec = (size_t)g * E.max_moves + mv;
-  for (int c = threadIdx.x; c < G::CELLS; c += kThreads) {
+  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     E.rec_stones[rec * G::CELLS + c] = sm.stone[c];
     E.rec_invd[rec * G::CELLS + c] = sm.invd[c];
   }

@@ -59,7 +59,7 @@ __device__ __forceinline__ double mask_of(const TreeLds<G>& t, int a) {
 template <class G, class InvdFn>
 __device__ __forceinline__ void build_mask(TreeLds<G>& t, double pass_epsilon, InvdFn invd) {
   int any = 0;
-  for (int a = threadIdx.x; a < G::A; a += kThreads) {
+  for (int a = threadIdx.x; a < G::A; a += G::THREADS) {
     uint8_t v = a < G::CELLS ? (invd(a) == 0 ? 1 : 0) : 1;
     t.valid[a] = v;
     any |= (a < G::CELLS) && v;
@@ -368,7 +368,7 @@ __device__ __forceinline__ void backup(const TreeView& T, int depth, int nid, do
 // Reset a tree to a bare root (children unexpanded, stats zero).  All threads.
 template <class G>
 __device__ __forceinline__ void tree_reset_root(const TreeView& T) {
-  for (int a = threadIdx.x; a < G::A; a += kThreads) T.child[a] = -1;
+  for (int a = threadIdx.x; a < G::A; a += G::THREADS) T.child[a] = -1;
   if (threadIdx.x == 0) { T.visits[0] = 0; T.wsum[0] = 0.0; }
 }
 
