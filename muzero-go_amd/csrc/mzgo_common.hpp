@@ -36,6 +36,7 @@ struct Geo {
   static constexpr int WAVES = NCG <= 2 ? 8 : 4;  // waves per workgroup
   static constexpr int THREADS = WAVES * 64;
   static constexpr int KSPLIT = WAVES / 4;        // conv k-range split over wave halves
+  static constexpr int TREE_CAP = NCG <= 2 ? 512 : 0;  // nodes whose stats fit in LDS (0: HBM only)
   static_assert(C % 16 == 0, "latent_dim must be a multiple of 16");
 };
 

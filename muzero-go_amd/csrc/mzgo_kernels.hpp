@@ -180,15 +180,16 @@ template <class G, class PlaneFn>
 __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                   const EngineArrays& E, int g, PlaneFn planes, const double* noise,
                                   uint64_t key) {
-  const TreeView T = TreeViewOf<G>::make(E, g);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
   float* pool = E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS;
   const size_t node_floats = (size_t)G::C * G::CS;
   const int S = sp.num_simulations;
+  TreeAcc<G> T(TV, sm.t, S + 2 <= G::TREE_CAP);
 
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
   tree_reset_root<G>(T);
   representation<G>(sm, np, planes, pool, G::CS);        // root latent -> node 0
-  if (wave_id() == 0) root_priors<G>(sm.t, T, sp, noise, key);
+  if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
   __syncthreads();
 
   int nodes = 1;
@@ -202,14 +203,14 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
     st.lap(0);
     const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;
     if (a < 0) {                                         // terminal leaf: backup 0 (:188-191)
-      if (threadIdx.x == 0) backup(T, depth, -1, 0.0);
+      if (wave_id() == 0) backup<G>(T, depth, -1, 0.0);
       __syncthreads();
       continue;
     }
     const int nid = nodes++;
-    int* crow = T.child + (size_t)nid * G::A;
+    int* crow = TV.child + (size_t)nid * G::A;
     for (int i = threadIdx.x; i < G::A; i += G::THREADS) crow[i] = -1;
-    if (threadIdx.x == 0) { T.visits[nid] = 0; T.wsum[nid] = 0.0; }
+    if (threadIdx.x == 0) T.init(nid);
     stage_board<G>(sm.u.in, pool + (size_t)leaf * node_floats, G::CS, G::C, np.emb + (size_t)a * G::C);
     __syncthreads();
     st.lap(1);
@@ -220,18 +221,19 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
     __syncthreads();
     st.lap(3);
     if (wave_id() == 0) {
-      child_priors<G>(sm.t, T.prior + (size_t)nid * G::A);
-      if (lane_id() == (a & 63)) T.child[(size_t)leaf * G::A + a] = nid;
+      child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A);
+      if (lane_id() == (a & 63)) T.set_child(leaf, a, nid);
     }
     __syncthreads();
     st.lap(4);
-    if (threadIdx.x == 0) {
+    if (wave_id() == 0) {
       const double v = (double)sm.t.reward + sp.discount * (double)sm.t.value;
-      backup(T, depth, nid, v);
+      backup<G>(T, depth, nid, v);
     }
     __syncthreads();
     st.lap(5);
   }
+  tree_flush<G>(T, nodes);
   if (threadIdx.x == 0) E.nodes[g] = nodes;
   __syncthreads();
 }

@@ -48,6 +48,47 @@ struct TreeLds {
   double pass_prior;       // 0.01 or 1.0
   float reward, value;
   int leaf, action, nid, depth, nodes, bcast;
+  // LDS-resident tree state (boards with G::TREE_CAP > 0 and S + 2 <= TREE_CAP)
+  int svis[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
+  double sws[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
+  int spath[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
+  int rchild[G::TREE_CAP > 0 ? G::A : 1];
+  double rprior[G::TREE_CAP > 0 ? G::A : 1];
+};
+
+// Tree accessor: node stats, path and the root's child row / priors either in
+// LDS (small boards, S + 2 <= TREE_CAP; copied back to HBM by flush()) or in
+// HBM.  Child rows / priors of non-root nodes always live in HBM.
+template <class G>
+struct TreeAcc {
+  TreeView T;
+  int* vis_;
+  double* ws_;
+  int* path_;
+  int* rchild_;       // LDS mirror of the root row, or null
+  double* rprior_;    // LDS mirror of the root priors, or null
+  __device__ __forceinline__ TreeAcc(const TreeView& tv, TreeLds<G>& t, bool lds) : T(tv) {
+    if (G::TREE_CAP > 0 && lds) {
+      vis_ = t.svis; ws_ = t.sws; path_ = t.spath; rchild_ = t.rchild; rprior_ = t.rprior;
+    } else {
+      vis_ = T.visits; ws_ = T.wsum; path_ = T.path; rchild_ = nullptr; rprior_ = nullptr;
+    }
+  }
+  __device__ __forceinline__ int vis(int n) const { return vis_[n]; }
+  __device__ __forceinline__ double ws(int n) const { return ws_[n]; }
+  __device__ __forceinline__ void add(int n, double dv) { vis_[n] += 1; ws_[n] = ws_[n] + dv; }
+  __device__ __forceinline__ void init(int n) { vis_[n] = 0; ws_[n] = 0.0; }
+  __device__ __forceinline__ int path(int i) const { return path_[i]; }
+  __device__ __forceinline__ void set_path(int i, int n) { path_[i] = n; }
+  __device__ __forceinline__ int child(int n, int a) const {
+    return (n == 0 && rchild_) ? rchild_[a] : T.child[(size_t)n * G::A + a];
+  }
+  __device__ __forceinline__ void set_child(int n, int a, int c) {
+    T.child[(size_t)n * G::A + a] = c;
+    if (n == 0 && rchild_) rchild_[a] = c;
+  }
+  __device__ __forceinline__ double root_prior(int a) const { return rprior_ ? rprior_[a] : T.root_prior[a]; }
+  __device__ __forceinline__ bool in_lds() const { return rchild_ != nullptr; }
 };
 
 template <class G>
@@ -241,6 +282,7 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
       const double m = mask_of<G>(t, a);
       const double p = s2 > 0.0 ? q[j] / s2 : m / ms;
       T.root_prior[a] = m > 0 ? p : 0.0;
+      if (G::TREE_CAP > 0) t.rprior[a] = m > 0 ? p : 0.0;   // LDS mirror (used if the tree is in LDS)
     }
   }
 }
@@ -251,16 +293,14 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 // (node ids, root first) is written to T.path[0..depth].
 // ---------------------------------------------------------------------------
 template <class G>
-__device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
+__device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, const SearchParams& sp,
                                   uint64_t key, int sim) {
   const int lane = lane_id();
   int node = 0, depth = 0;
-  if (lane == 0) T.path[0] = 0;
   for (int guard = 0; guard <= sp.num_simulations + 1; ++guard) {
     const bool root = node == 0;
-    const int nvis = T.visits[node];
-    const int* ch_row = T.child + (size_t)node * G::A;
-    const float* pr_row = T.prior + (size_t)node * G::A;
+    const int nvis = T.vis(node);
+    const float* pr_row = T.T.prior + (size_t)node * G::A;
     double P[G::AP];
     int ch[G::AP];
     uint64_t anypos = 0, elig[G::AP], unexp[G::AP];
@@ -269,8 +309,8 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, con
     for (int j = 0; j < G::AP; ++j) {
       const int a = lane + 64 * j;
       const bool in = a < G::A;
-      P[j] = in ? (root ? T.root_prior[a] : (double)pr_row[a]) : 0.0;
-      ch[j] = in ? ch_row[a] : -1;
+      P[j] = in ? (root ? T.root_prior(a) : (double)pr_row[a]) : 0.0;
+      ch[j] = in ? T.child(node, a) : -1;
       const bool pos = in && P[j] > 0.0;
       const bool e = pos && mask_of<G>(t, a) > 0.0;
       anypos |= __ballot(pos);
@@ -313,8 +353,8 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, con
       n[j] = 0;
       if ((elig[j] >> lane) & 1ull) {
         const int c = ch[j];
-        n[j] = T.visits[c];
-        q[j] = n[j] > 0 ? T.wsum[c] / (double)n[j] : 0.0;
+        n[j] = T.vis(c);
+        q[j] = n[j] > 0 ? T.ws(c) / (double)n[j] : 0.0;
         lo = fmin(lo, q[j]);
         hi = fmax(hi, q[j]);
       }
@@ -323,7 +363,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, con
     hi = wave_max(hi);
     const double sq = sqrt((double)(nvis > 1 ? nvis : 1));
     double best_s = -INFINITY;
-    int best_a = 0x7fffffff;
+    int best_a = 0x7fffffff, best_c = -1;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
       const int a = lane + 64 * j;
@@ -333,20 +373,20 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, con
         if (root) u = ((sp.c_puct * P[j]) * sq) / (double)(1 + n[j]);
         else u = ((double)((float)sp.c_puct * (float)P[j]) * sq) / (double)(1 + n[j]);
         const double sc = qn + u;
-        if (sc > best_s || (sc == best_s && a < best_a)) { best_s = sc; best_a = a; }
+        if (sc > best_s || (sc == best_s && a < best_a)) { best_s = sc; best_a = a; best_c = ch[j]; }
       }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const double os = __shfl_xor(best_s, o);
       const int oa = __shfl_xor(best_a, o);
-      if (os > best_s || (os == best_s && oa < best_a)) { best_s = os; best_a = oa; }
+      const int oc = __shfl_xor(best_c, o);
+      if (os > best_s || (os == best_s && oa < best_a)) { best_s = os; best_a = oa; best_c = oc; }
     }
     if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return -1; }
-    const int nxt = T.child[(size_t)node * G::A + best_a];
     depth += 1;
-    if (lane == 0) T.path[depth] = nxt;
-    node = nxt;
+    if (lane == 0) T.path_[depth] = best_c;
+    node = best_c;
   }
   t.leaf = node;
   t.depth = depth;
@@ -354,22 +394,35 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeView& T, con
 }
 
 // Backup along path[0..depth] (+ the new node nid if >= 0): leaf-most gets
-// +v, alternating sign upward (self_play.py:337-343).  Lane 0 of wave 0.
-__device__ __forceinline__ void backup(const TreeView& T, int depth, int nid, double v) {
-  int i = 0;
-  if (nid >= 0) { T.visits[nid] += 1; T.wsum[nid] = T.wsum[nid] + v; i = 1; }
-  for (int d = depth; d >= 0; --d, ++i) {
-    const int node = T.path[d];
-    T.visits[node] += 1;
-    T.wsum[node] = T.wsum[node] + ((i & 1) ? -v : v);
+// +v, alternating sign upward (self_play.py:337-343).  Wave 0; path nodes are
+// distinct, so each lane updates its own node.  Path entry 0 is the root.
+template <class G>
+__device__ __forceinline__ void backup(TreeAcc<G>& T, int depth, int nid, double v) {
+  const int lane = lane_id();
+  const int off = nid >= 0 ? 1 : 0;
+  const int count = depth + 1 + off;              // nodes on the backed-up path
+  for (int i = lane; i < count; i += 64) {
+    const int node = (off && i == 0) ? nid : T.path(depth - (i - off));
+    T.add(node, (i & 1) ? -v : v);
   }
+  wave_lds_sync();
 }
 
 // Reset a tree to a bare root (children unexpanded, stats zero).  All threads.
 template <class G>
-__device__ __forceinline__ void tree_reset_root(const TreeView& T) {
-  for (int a = threadIdx.x; a < G::A; a += G::THREADS) T.child[a] = -1;
-  if (threadIdx.x == 0) { T.visits[0] = 0; T.wsum[0] = 0.0; }
+__device__ __forceinline__ void tree_reset_root(TreeAcc<G>& T) {
+  for (int a = threadIdx.x; a < G::A; a += G::THREADS) T.set_child(0, a, -1);
+  if (threadIdx.x == 0) { T.init(0); T.set_path(0, 0); }
+}
+
+// Write LDS-resident stats of nodes [0, nodes) back to HBM.  All threads.
+template <class G>
+__device__ __forceinline__ void tree_flush(TreeAcc<G>& T, int nodes) {
+  if (!T.in_lds()) return;
+  for (int n = threadIdx.x; n < nodes; n += G::THREADS) {
+    T.T.visits[n] = T.vis_[n];
+    T.T.wsum[n] = T.ws_[n];
+  }
 }
 
 }  // namespace mzgo
