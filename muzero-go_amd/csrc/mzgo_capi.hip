@@ -101,6 +101,44 @@ std::vector<float> pack_conv(const float* W, int COUT, int CIN, bool cog_major, 
   return out;
 }
 
+// conv weight W[cout][cin][3][3] -> Winograd U for mzgo_wino.hpp (9x9):
+// U_xi[cout][cin] = (G2 g G3^T)[i][j], g = W[cout][cin], xi = i*5 + j, with
+// G2 of F(2,3) (points 0, 1, -1, inf) on kernel rows and G3 of F(3,3)
+// (points 0, 1, -1, -2, inf) on kernel columns, computed in double and
+// rounded once.  Packed as packed[(((m*2 + h)*L + pos)*64 + lane)*4 + e]
+// = U_xi[16m + (lane & 15)][hh*CIN/2 + 4*(4*s4 + e) + (lane >> 4)] for
+// xi = h*10 + xl, k-position k = hh*S4 + s4 (S4 = CIN/32), and
+// pos = ((xl/XG)*KP + k)*XG + xl%XG (kWinoXG, KP = CIN/16): one contiguous
+// float4 stream per (cout tile m, xi half h) wave, in the order wino_conv
+// consumes it.
+std::vector<float> pack_wino(const float* W, int COUT, int CIN) {
+  static const double G2[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  static const double G3[5][3] = {{0.5, 0, 0},
+                                  {1.0 / 6, 1.0 / 6, 1.0 / 6},
+                                  {0.5, -0.5, 0.5},
+                                  {1.0 / 6, -1.0 / 3, 2.0 / 3},
+                                  {0, 0, 1}};
+  const int MT = COUT / 16, CH = CIN / 2, S4 = CH / 16, KP = CIN / 16, L = 10 * KP;
+  std::vector<float> out((size_t)MT * 2 * L * 64 * 4, 0.f);
+  for (int m = 0; m < MT; ++m)
+    for (int h = 0; h < 2; ++h)
+      for (int xl = 0; xl < 10; ++xl)
+        for (int k = 0; k < KP; ++k)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int e = 0; e < 4; ++e) {
+              const int xi = h * 10 + xl, i = xi / 5, j = xi % 5;
+              const int hh = k / S4, s4 = k % S4;
+              const int co = 16 * m + (lane & 15), ci = hh * CH + 4 * (4 * s4 + e) + (lane >> 4);
+              const float* g = W + ((size_t)co * CIN + ci) * 9;
+              double u = 0.0;
+              for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) u += G2[i][a] * (double)g[a * 3 + b] * G3[j][b];
+              const int pos = ((xl / kWinoXG) * KP + k) * kWinoXG + xl % kWinoXG;  // consumption order
+              out[((((size_t)m * 2 + h) * L + pos) * 64 + lane) * 4 + e] = (float)u;
+            }
+  return out;
+}
+
 }  // namespace
 
 struct mzgo_engine {
@@ -147,11 +185,15 @@ struct mzgo_engine {
     // k-range split of the ring conv: 2 when the board runs 8 waves (Geo::KSPLIT)
     const int ct = (N * N + 15) / 16, ng = ct >= 3 ? 3 : ct, ncg = (ct + ng - 1) / ng;
     const int ksplit = ncg <= 2 ? 2 : 1;
-    parts.push_back(pack_conv(sd["representation.conv2.weight"].data(), 64, 64, true, ksplit));
+    const bool wino = N == 9;                      // Geo::WINO
+    auto latent = [&](const char* key, int cout, int cin) {
+      return wino ? pack_wino(sd[key].data(), cout, cin) : pack_conv(sd[key].data(), cout, cin, true, ksplit);
+    };
+    parts.push_back(latent("representation.conv2.weight", 64, 64));
     parts.push_back(sd["representation.conv2.bias"]);
-    parts.push_back(pack_conv(sd["representation.conv3.weight"].data(), C, 64, true, ksplit));
+    parts.push_back(latent("representation.conv3.weight", C, 64));
     parts.push_back(sd["representation.conv3.bias"]);
-    parts.push_back(pack_conv(sd["dynamics.conv.weight"].data(), C, C, true, ksplit));
+    parts.push_back(latent("dynamics.conv.weight", C, C));
     parts.push_back(sd["dynamics.conv.bias"]);
     parts.push_back(sd["dynamics.action_embedding.weight"]);
     std::vector<float> hw;
@@ -251,6 +293,9 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   auto chk = [&](int r) { if (r != MZGO_OK && rc == MZGO_OK) rc = r; };
   if (C != 0) {
     chk(e->alloc(&E.pool, G * n1 * (size_t)C * e->CS));
+    // pad cells (>= N*N) of pooled latents are read as zeros and never written
+    if (rc == MZGO_OK && hipMemset(E.pool, 0, G * n1 * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
+      chk(fail(MZGO_EHIP, "hipMemset(pool) failed"));
     chk(e->alloc(&E.prior, G * n1 * A));
     chk(e->alloc(&E.child, G * n1 * A));
     chk(e->alloc(&E.visits, G * n1));

@@ -10,9 +10,10 @@
 
 namespace mzgo {
 
-// One workgroup per game.  Boards with one cell job per cout group (5x5, 6x6,
-// 9x9) run 8 waves = 2 per SIMD, the wave pairs splitting the conv k-range;
-// 19x19 runs 4 waves (its 4 cell jobs per wave need every register).
+// One workgroup per game.  9x9 runs 12 waves = 3 per SIMD (Winograd convs,
+// one wave per cout tile and cin half); 5x5 and 6x6 run 8 waves = 2 per SIMD,
+// the wave pairs splitting the direct conv's k-range; 19x19 runs 4 waves (its
+// 4 cell jobs per wave need every register).
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -33,9 +34,12 @@ struct Geo {
   static constexpr int NG = CT >= 3 ? 3 : CT;     // cell tiles per wave job
   static constexpr int NCG = (CT + NG - 1) / NG;  // cell groups
   static constexpr int AP = (A + 63) / 64;        // actions per lane (a = lane + 64*j)
-  static constexpr int WAVES = NCG <= 2 ? 8 : 4;  // waves per workgroup
+  // 9x9 runs its latent convs as Winograd F(2,3)xF(3,3) GEMMs (mzgo_wino.hpp)
+  static constexpr bool WINO = N == 9;
+  static constexpr int WAVES = WINO ? 12 : (NCG <= 2 ? 8 : 4);  // waves per workgroup
   static constexpr int THREADS = WAVES * 64;
-  static constexpr int KSPLIT = WAVES / 4;        // conv k-range split over wave halves
+  static constexpr int WPE = WAVES / 4;           // waves per SIMD
+  static constexpr int KSPLIT = WINO ? 2 : WAVES / 4;  // ring conv: k-range split over wave halves
   static constexpr int TREE_CAP = NCG <= 2 ? 512 : 0;  // nodes whose stats fit in LDS (0: HBM only)
   static_assert(C % 16 == 0, "latent_dim must be a multiple of 16");
 };
@@ -69,7 +73,7 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // scripts/microbench.py).  Thread 0 of each workgroup adds shader-clock
 // deltas per phase into mzgo_stamps[block][phase].
 // ---------------------------------------------------------------------------
-constexpr int kStampPhases = 8;
+constexpr int kStampPhases = 24;   // 0-7 phases (thread 0), 8-19 per-wave conv loops
 #ifdef MZGO_STAMPS
 struct Stamp {
   unsigned long long* buf;
@@ -80,11 +84,15 @@ struct Stamp {
     if (buf && threadIdx.x == 0) buf[blockIdx.x * kStampPhases + phase] += now - t;
     t = now;
   }
+  __device__ void wave_add(int phase, unsigned long long cycles) {
+    if (buf && (threadIdx.x & 63) == 0) buf[blockIdx.x * kStampPhases + phase] += cycles;
+  }
 };
 #else
 struct Stamp {
   __device__ explicit Stamp(unsigned long long*) {}
   __device__ void lap(int) {}
+  __device__ void wave_add(int, unsigned long long) {}
 };
 #endif
 

@@ -426,13 +426,30 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
     }
   }
   if (st) st->lap(6);
+  // The epilogue is run by the LAST k-half (EPI): with KSPLIT == 2 that keeps
+  // waves 0-3, which run the tree phases, free of outstanding HBM stores
+  // (a later load's vmcnt wait would wait for their acks).  Its bias and head
+  // weights are loaded here, before any store is issued, for the same reason.
+  constexpr int EPI = KSPLIT - 1;
+  float bb[MG][4], hw[NH > 0 ? NH : 1][MG][4];
+  if (active && half == EPI) {
+#pragma unroll
+    for (int mi = 0; mi < MG; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (cog * MG + mi) * 16 + kq * 4 + r;
+        bb[mi][r] = bias[co];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) hw[h][mi][r] = head_w[h * COUT + co];
+      }
+  }
   __syncthreads();   // every wave is done with lds_in and its ring
   if constexpr (KSPLIT == 2) {
-    // second k-half hands its partial accumulators to its partner through the
-    // (now idle) rings; the first half adds them in a fixed order
+    // the first k-half hands its partial accumulators to its partner through
+    // the (now idle) rings; the second half adds them (a + b == b + a)
     float* red = ring + wl * (JW * MG * NG * 4 * 64);
     static_assert(4 * JW * MG * NG * 4 * 64 * 4 <= RingBytes<G>::value, "reduction fits the rings");
-    if (half == 1 && active) {
+    if (half == 0 && active) {
 #pragma unroll
       for (int j = 0; j < JW; ++j)
 #pragma unroll
@@ -443,7 +460,7 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
             for (int r = 0; r < 4; ++r) red[(((j * MG + mi) * NG + ni) * 4 + r) * 64 + lane] = acc[j][mi][ni][r];
     }
     __syncthreads();
-    if (half == 0 && active) {
+    if (half == 1 && active) {
 #pragma unroll
       for (int j = 0; j < JW; ++j)
 #pragma unroll
@@ -464,28 +481,24 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
     for (int j = 0; j < JW; ++j)
 #pragma unroll
       for (int ni = 0; ni < NG; ++ni) hsum[h][j][ni] = 0.f;
-  if (active && half == 0) {
+  if (active && half == EPI) {
 #pragma unroll
     for (int mi = 0; mi < MG; ++mi) {
       const int cout0 = (cog * MG + mi) * 16 + kq * 4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = cout0 + r;
-        const float bb = bias[co];
-        float hw[NH > 0 ? NH : 1];
-#pragma unroll
-        for (int h = 0; h < NH; ++h) hw[h] = head_w[h * COUT + co];
 #pragma unroll
         for (int j = 0; j < JW; ++j) {
 #pragma unroll
           for (int ni = 0; ni < NG; ++ni) {
-            float v = acc[j][mi][ni][r] + bb;
+            float v = acc[j][mi][ni][r] + bb[mi][r];
             v = v > 0.f ? v : 0.f;
             const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
             v = cell < G::CELLS ? v : 0.f;                  // pad cells stay 0 (zero slot)
             if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
 #pragma unroll
-            for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h], v, hsum[h][j][ni]);
+            for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h][mi][r], v, hsum[h][j][ni]);
           }
         }
       }

@@ -7,6 +7,7 @@
 #include "mzgo_board.hpp"
 #include "mzgo_conv.hpp"
 #include "mzgo_search.hpp"
+#include "mzgo_wino.hpp"
 
 namespace mzgo {
 
@@ -68,8 +69,8 @@ struct TreeViewOf {
   }
 };
 
-// LDS of one game's workgroup.
-template <class G>
+// LDS of one game's workgroup: direct-conv boards (weight DMA rings) ...
+template <class G, bool W = G::WINO>
 struct Smem {
   union alignas(16) {
     float in[G::CINMAX * G::CPAD];                       // conv staging
@@ -83,7 +84,52 @@ struct Smem {
   int killed[4];
   int misc[8];
   int bc[8];                                             // broadcast slots
+  __device__ float* heads() { return u.hp; }
+  static constexpr int HEAD_PARTS = ConvShape<G::C>::NCOG;
 };
+
+// ... and Winograd boards (transformed input; exchange buffer + head partials)
+template <class G>
+struct Smem<G, true> {
+  union alignas(16) {
+    float in[8 * G::CPAD];                               // conv1 input (6 planes + 2 zero)
+    float v[Wino<G>::template v_floats<G::CINMAX>()];    // transformed conv input
+    struct {
+      float red[Wino<G>::template red_floats<G::C>()];
+      float hp[(G::C / 16) * 3 * G::CS];
+    } x;
+    struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
+  } u;
+  alignas(16) float raw[WinoRaw<G>::CH_MAX * WinoRaw<G>::STRIDE];  // one cin half of the conv input
+  TreeLds<G> t;
+  int8_t stone[G::CELLS];
+  uint8_t invd[G::CELLS];
+  int killed[4];
+  int misc[8];
+  int bc[8];
+  __device__ float* heads() { return u.x.hp; }
+  static constexpr int HEAD_PARTS = G::C / 16;
+};
+
+// One latent conv: src ([CIN][src_stride], global) (+ emb per channel) ->
+// dst ([COUT][dst_stride], cells < out_cells), NH fused 1x1 head partials left
+// in sm.heads().  All threads; returns synchronised.
+template <class G, int CIN, int COUT, int NH>
+__device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict__ w, const float* __restrict__ b,
+                                            const float* src, int src_stride, const float* emb, float* dst,
+                                            int dst_stride, int out_cells, const float* head_w,
+                                            Stamp* st = nullptr) {
+  if constexpr (G::WINO) {
+    wino_input<G, CIN>(sm.u.v, sm.raw, src, src_stride, emb, st);
+    if (st) st->lap(1);
+    wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, w, b, dst, dst_stride, out_cells, head_w, st);
+  } else {
+    stage_board<G>(sm.u.in, src, src_stride, CIN, emb);
+    __syncthreads();
+    if (st) st->lap(1);
+    conv3x3_ring<G, CIN, COUT, NH>(sm.u.in, sm.ring, w, b, dst, dst_stride, out_cells, head_w, sm.u.hp, st);
+  }
+}
 
 template <class G>
 __device__ __forceinline__ BoardLds<G> board_lds(Smem<G>& sm) {
@@ -108,20 +154,17 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
     sm.u.in[c * G::CPAD + j] = planes(c, j);
   }
   zero_channels<G>(sm.u.in, 6, 8);
+  stage_head_scalars(np.hs, sm.t.hsc);
   __syncthreads();
-  HeadPart<G> hp{sm.u.hp};
+  HeadPart<G> hp{nullptr};
   const int oc = lat_stride == G::CS ? G::CS : G::CELLS;   // pooled latents also write their 0 pads
   conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
   __syncthreads();
-  stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
-  __syncthreads();
-  conv3x3_ring<G, 64, 64, 0>(sm.u.in, sm.ring, np.w_conv2, np.b_conv2, lat, lat_stride, oc,
-                             nullptr, sm.u.hp);
-  stage_board<G>(sm.u.in, lat, lat_stride, 64, nullptr);
-  __syncthreads();
-  conv3x3_ring<G, 64, G::C, 2>(sm.u.in, sm.ring, np.w_conv3, np.b_conv3, lat, lat_stride, oc,
-                               np.head_w + G::C, sm.u.hp);
-  if (wave_id() == 0) finalize_heads<G>(sm.u.hp, false, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+  latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, lat, lat_stride, oc, nullptr);
+  latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, lat, lat_stride, nullptr, lat, lat_stride, oc,
+                              np.head_w + G::C);
+  if (wave_id() == 0)
+    finalize_heads<G, Smem<G>::HEAD_PARTS>(sm.heads(), false, sm.t.hsc, sm.t.logits, &sm.t.reward, &sm.t.value);
   __syncthreads();
 }
 
@@ -130,11 +173,11 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
 template <class G>
 __device__ __forceinline__ void dynamics(Smem<G>& sm, const NetParams& np, const float* src, int src_stride,
                                 int action, float* dst, int dst_stride) {
-  stage_board<G>(sm.u.in, src, src_stride, G::C, np.emb + (size_t)action * G::C);
-  __syncthreads();
-  conv3x3_ring<G, G::C, G::C, 3>(sm.u.in, sm.ring, np.w_dyn, np.b_dyn, dst, dst_stride,
-                                 dst_stride == G::CS ? G::CS : G::CELLS, np.head_w, sm.u.hp);
-  if (wave_id() == 0) finalize_heads<G>(sm.u.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
+  stage_head_scalars(np.hs, sm.t.hsc);
+  latent_conv<G, G::C, G::C, 3>(sm, np.w_dyn, np.b_dyn, src, src_stride, np.emb + (size_t)action * G::C, dst,
+                                dst_stride, dst_stride == G::CS ? G::CS : G::CELLS, np.head_w);
+  if (wave_id() == 0)
+    finalize_heads<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, sm.t.logits, &sm.t.reward, &sm.t.value);
   __syncthreads();
 }
 
@@ -142,7 +185,7 @@ __device__ __forceinline__ void dynamics(Smem<G>& sm, const NetParams& np, const
 // Batched drop-in inference (self_play.py:121-128)
 // ---------------------------------------------------------------------------
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_initial_inference(NetParams np, const float* __restrict__ obs,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_initial_inference(NetParams np, const float* __restrict__ obs,
                                                                  float* latent, float* value, float* logits) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -155,7 +198,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_recurrent_inference(NetParams np, const float* __restrict__ latent,
                                                                    const int64_t* __restrict__ action,
                                                                    float* next_latent, float* reward,
                                                                    float* value, float* logits, int* err) {
@@ -188,6 +231,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
 
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
   tree_reset_root<G>(T);
+  if (threadIdx.x == 0) { sm.t.newest = -1; sm.t.newp_node = -1; }
   representation<G>(sm, np, planes, pool, G::CS);        // root latent -> node 0
   if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
   __syncthreads();
@@ -208,31 +252,30 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
       continue;
     }
     const int nid = nodes++;
-    int* crow = TV.child + (size_t)nid * G::A;
-    for (int i = threadIdx.x; i < G::A; i += G::THREADS) crow[i] = -1;
-    if (threadIdx.x == 0) T.init(nid);
-    stage_board<G>(sm.u.in, pool + (size_t)leaf * node_floats, G::CS, G::C, np.emb + (size_t)a * G::C);
-    __syncthreads();
-    st.lap(1);
-    conv3x3_ring<G, G::C, G::C, 3>(sm.u.in, sm.ring, np.w_dyn, np.b_dyn, pool + (size_t)nid * node_floats,
-                                   G::CS, G::CS, np.head_w, sm.u.hp, &st);
+    if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
+    latent_conv<G, G::C, G::C, 3>(sm, np.w_dyn, np.b_dyn, pool + (size_t)leaf * node_floats, G::CS,
+                                  np.emb + (size_t)a * G::C, pool + (size_t)nid * node_floats, G::CS, G::CS,
+                                  np.head_w, &st);
     st.lap(2);
-    if (wave_id() == 0) finalize_heads<G>(sm.u.hp, true, np.hs, sm.t.logits, &sm.t.reward, &sm.t.value);
-    __syncthreads();
-    st.lap(3);
+    // wave 1: policy logits -> the new node's priors (published in LDS for a
+    // select that reaches it); wave 0, meanwhile: value/reward heads, backup
+    // and (next iteration) the next select.  Wave 0 issues no HBM stores, so
+    // its tree loads never wait for store acks.  The select barrier joins them.
+    if (wave_id() == 1) {
+      heads_logits<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, sm.t.logits);
+      child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A, nid);
+      int* crow = TV.child + (size_t)nid * G::A;      // the new node: no children yet
+      for (int i = lane_id(); i < G::A; i += 64) crow[i] = -1;
+    }
     if (wave_id() == 0) {
-      child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A);
+      float r, v;
+      heads_value<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, r, v);
       if (lane_id() == (a & 63)) T.set_child(leaf, a, nid);
+      backup<G>(T, depth, nid, (double)r + sp.discount * (double)v);
     }
-    __syncthreads();
-    st.lap(4);
-    if (wave_id() == 0) {
-      const double v = (double)sm.t.reward + sp.discount * (double)sm.t.value;
-      backup<G>(T, depth, nid, v);
-    }
-    __syncthreads();
-    st.lap(5);
+    st.lap(3);
   }
+  __syncthreads();
   tree_flush<G>(T, nodes);
   if (threadIdx.x == 0) E.nodes[g] = nodes;
   __syncthreads();
@@ -253,7 +296,7 @@ __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_search(NetParams np, SearchParams sp, EngineArrays E,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_search(NetParams np, SearchParams sp, EngineArrays E,
                                                       const float* __restrict__ root_obs,
                                                       const double* __restrict__ noise, int game_base,
                                                       int move_index, int* out_visits, double* out_value) {
@@ -306,7 +349,7 @@ __device__ __forceinline__ float board_plane(const Smem<G>& sm, const BoardMeta&
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_board_reset(EngineArrays E) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_board_reset(EngineArrays E) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
   for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
@@ -320,7 +363,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 // Step every slot with actions[g] >= 0 (gogame.next_state); status[g] gets a
 // BOARD_* code; winner[g] = GoEnv.winner() after the step (0 unless ended).
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_board_step(EngineArrays E, const int* __restrict__ actions,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_board_step(EngineArrays E, const int* __restrict__ actions,
                                                           int* status, double* winner, double komi) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -343,7 +386,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 
 // f64 observation planes [G][6][CELLS] of the current boards (GoEnv state)
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_board_planes(EngineArrays E, double* planes) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_board_planes(EngineArrays E, double* planes) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
   const int* mm = E.meta + g * 4;
@@ -471,7 +514,7 @@ struct PlayParams {
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::KSPLIT, Geo<N, C>::KSPLIT))) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
                                                              EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;

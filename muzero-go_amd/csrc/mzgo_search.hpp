@@ -48,12 +48,18 @@ struct TreeLds {
   double pass_prior;       // 0.01 or 1.0
   float reward, value;
   int leaf, action, nid, depth, nodes, bcast;
+  float hsc[64];                   // staged HeadScalars (HS_* offsets)
   // LDS-resident tree state (boards with G::TREE_CAP > 0 and S + 2 <= TREE_CAP)
   int svis[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
   double sws[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
   int spath[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
   int rchild[G::TREE_CAP > 0 ? G::A : 1];
   double rprior[G::TREE_CAP > 0 ? G::A : 1];
+  // priors of the newest node, written by wave 1 while wave 0 backs up and
+  // selects the next leaf; select waits on newp_node only if it reaches it
+  float newp[G::A];
+  int newest;              // id of the newest node (-1: none)
+  int newp_node;           // node whose priors newp holds (atomic, workgroup scope)
 };
 
 // Tree accessor: node stats, path and the root's child row / priors either in
@@ -141,42 +147,92 @@ struct HeadScalars {
   const float* pass_logit;  // [1]
 };
 
-template <class G>
-__device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward, const HeadScalars& hs,
-                                      float* logits, float* reward, float* value) {
+// HeadScalars staged in LDS (one load round per kernel instead of one per
+// simulation): offsets into TreeLds::hsc.
+enum : int { HS_RB = 0, HS_FC1W = 1, HS_FC1B = 17, HS_FC2W = 33, HS_FC2B = 49, HS_VB = 50, HS_VFCW = 51,
+             HS_VFCB = 52, HS_PB = 53, HS_PASS = 54, HS_COUNT = 55 };
+
+// All threads; visible after the caller's next barrier.
+__device__ __forceinline__ void stage_head_scalars(const HeadScalars& hs, float* dst) {
+  const int i = threadIdx.x;
+  if (i >= HS_COUNT) return;
+  const float* src;
+  if (i == HS_RB) src = hs.reward_b;
+  else if (i < HS_FC1B) src = hs.fc1_w + (i - HS_FC1W);
+  else if (i < HS_FC2W) src = hs.fc1_b + (i - HS_FC1B);
+  else if (i < HS_FC2B) src = hs.fc2_w + (i - HS_FC2W);
+  else if (i == HS_FC2B) src = hs.fc2_b;
+  else if (i == HS_VB) src = hs.value_b;
+  else if (i == HS_VFCW) src = hs.vfc_w;
+  else if (i == HS_VFCB) src = hs.vfc_b;
+  else if (i == HS_PB) src = hs.policy_b;
+  else src = hs.pass_logit;
+  dst[i] = *src;
+}
+
+// hp: [NPART][3][CS] partial sums over cout groups, added in a fixed order
+template <class G, int NPART>
+__device__ __forceinline__ float head_at(const float* hp, int h, int c) {
+  float s = hp[h * G::CS + c];
+#pragma unroll
+  for (int p = 1; p < NPART; ++p) s += hp[(p * 3 + h) * G::CS + c];
+  return s;
+}
+
+// value (and reward) heads; returns them on every lane.  One wave.
+template <class G, int NPART>
+__device__ __forceinline__ void heads_value(const float* hp, bool has_reward, const float* hsc, float& reward,
+                                            float& value) {
   const int lane = lane_id();
-  const int hv = has_reward ? 1 : 0, hpol = hv + 1;
-  auto head = [&](int h, int c) { return hp[h * G::CS + c] + hp[(3 + h) * G::CS + c]; };
-  const float vb = hs.value_b[0], pb = hs.policy_b[0];
+  const int hv = has_reward ? 1 : 0;
+  const float vb = hsc[HS_VB];
   float vs = 0.f, rs = 0.f;
-  const float rb = has_reward ? hs.reward_b[0] : 0.f;
+  const float rb = has_reward ? hsc[HS_RB] : 0.f;
   for (int c = lane; c < G::CELLS; c += 64) {
-    vs += head(hv, c) + vb;
-    if (has_reward) rs += head(0, c) + rb;
-    logits[c] = head(hpol, c) + pb;
+    vs += head_at<G, NPART>(hp, hv, c) + vb;
+    if (has_reward) rs += head_at<G, NPART>(hp, 0, c) + rb;
   }
-  if (lane == 0) logits[G::CELLS] = hs.pass_logit[0];
   vs = wave_sum(vs);
   const float vmean = vs / (float)G::CELLS;
-  if (lane == 0) *value = vmean * hs.vfc_w[0] + hs.vfc_b[0];
+  value = vmean * hsc[HS_VFCW] + hsc[HS_VFCB];
+  reward = 0.f;
   if (has_reward) {
     rs = wave_sum(rs);
     const float rmean = rs / (float)G::CELLS;
     float h = 0.f;
     if (lane < 16) {
-      h = rmean * hs.fc1_w[lane] + hs.fc1_b[lane];
+      h = rmean * hsc[HS_FC1W + lane] + hsc[HS_FC1B + lane];
       h = h > 0.f ? h : 0.f;
-      h = h * hs.fc2_w[lane];
+      h = h * hsc[HS_FC2W + lane];
     }
     h = wave_sum(h);
-    if (lane == 0) *reward = h + hs.fc2_b[0];
+    reward = h + hsc[HS_FC2B];
   }
+}
+
+// policy logits (cells, then the learned pass logit).  One wave.
+template <class G, int NPART>
+__device__ __forceinline__ void heads_logits(const float* hp, bool has_reward, const float* hsc, float* logits) {
+  const int lane = lane_id();
+  const int hpol = has_reward ? 2 : 1;
+  const float pb = hsc[HS_PB];
+  for (int c = lane; c < G::CELLS; c += 64) logits[c] = head_at<G, NPART>(hp, hpol, c) + pb;
+  if (lane == 0) logits[G::CELLS] = hsc[HS_PASS];
+}
+
+template <class G, int NPART>
+__device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward, const float* hsc,
+                                      float* logits, float* reward, float* value) {
+  float r, v;
+  heads_value<G, NPART>(hp, has_reward, hsc, r, v);
+  heads_logits<G, NPART>(hp, has_reward, hsc, logits);
+  if (lane_id() == 0) { *value = v; *reward = r; }
 }
 
 // Child priors of a new node (self_play.py:204-224): p = softmax * root mask,
 // normalised by numpy's f32 pairwise sum; entries with mask 0 are 0.  Wave 0.
 template <class G>
-__device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst) {
+__device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst, int node = -1) {
   const int lane = lane_id();
   softmax_wave<G>(t);
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
@@ -184,15 +240,24 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ 
   if (s > 0.f) {
     for (int a = lane; a < G::A; a += 64) {
       const double m = mask_of<G>(t, a);
-      dst[a] = m > 0 ? t.fbuf[a] / s : 0.f;
+      const float p = m > 0 ? t.fbuf[a] / s : 0.f;
+      dst[a] = p;
+      if (node >= 0) t.newp[a] = p;
     }
   } else {
     // fallback of :215 (uniform over the mask; the reference's f64 here is
     // stored as f32 -- unreachable unless every valid softmax entry underflows)
     for (int a = lane; a < G::A; a += 64) t.dbuf[a] = mask_of<G>(t, a);
     const double ms = np_pairwise_sum<double, G::A>(t.dbuf);
-    for (int a = lane; a < G::A; a += 64) dst[a] = (float)(mask_of<G>(t, a) / ms);
+    for (int a = lane; a < G::A; a += 64) {
+      const float p = (float)(mask_of<G>(t, a) / ms);
+      dst[a] = p;
+      if (node >= 0) t.newp[a] = p;
+    }
   }
+  // publish newp for a select running concurrently on another wave
+  if (node >= 0 && lane == 0)
+    __hip_atomic_store(&t.newp_node, node, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Gamma(alpha) by Marsaglia-Tsang with the alpha+1 boost, from the counter
@@ -301,6 +366,11 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
     const bool root = node == 0;
     const int nvis = T.vis(node);
     const float* pr_row = T.T.prior + (size_t)node * G::A;
+    // the newest node's priors may still be in the making (wave 1)
+    const bool fresh = !root && node == t.newest;
+    if (fresh)
+      while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != node)
+        __builtin_amdgcn_s_sleep(1);
     double P[G::AP];
     int ch[G::AP];
     uint64_t anypos = 0, elig[G::AP], unexp[G::AP];
@@ -309,7 +379,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
     for (int j = 0; j < G::AP; ++j) {
       const int a = lane + 64 * j;
       const bool in = a < G::A;
-      P[j] = in ? (root ? T.root_prior(a) : (double)pr_row[a]) : 0.0;
+      P[j] = in ? (root ? T.root_prior(a) : (double)(fresh ? t.newp[a] : pr_row[a])) : 0.0;
       ch[j] = in ? T.child(node, a) : -1;
       const bool pos = in && P[j] > 0.0;
       const bool e = pos && mask_of<G>(t, a) > 0.0;

@@ -1,0 +1,374 @@
+// mzgo_wino.hpp -- the 3x3/pad-1 convolution of one 9x9 board as a Winograd
+// F(2,3) x F(3,3) transform on fp32 MFMA (v_mfma_f32_16x16x4_f32), with the
+// MuZero heads fused into the epilogue.
+//
+// Rows use F(2,3) (points 0, 1, -1, inf), columns F(3,3) (points 0, 1, -1,
+// -2, inf): a 9x9 board is 5 x 3 = 15 output tiles of 2 x 3 cells, so the
+// tile index fills one 16-column MFMA tile, and the conv becomes 20 GEMMs
+//     M_xi[cout][tile] = sum_cin U_xi[cout][cin] * V_xi[cin][tile],  xi = (i, j)
+// of 96 x 96 x 16 -- 2880 MFMAs per conv instead of 7776 for the direct
+// implicit GEMM over 96 padded cells.  The device transforms are integer
+// (BT, AT below); the fractions of G live in U, packed by the host
+// (mzgo_capi.hip: pack_wino).  fp32 error is on par with the direct conv
+// (the per-output sums run over 96 inputs instead of 864).
+//
+// Work split: 12 waves (3 per SIMD); wave w owns cout tile m = w / 2 and xi
+// half h = w % 2 (xi rows i = 2h, 2h + 1; all cin), so each M_xi is computed
+// and folded into the output transform once; A (U) is streamed straight from
+// L2 into VGPRs -- nothing but the transformed input lives in LDS.  The two
+// xi halves exchange half of their transformed outputs through LDS: wave h
+// finalises output row oy = h of each tile.
+//
+// Replaces the torch conv2d calls of self_play.py:72-74 (representation
+// conv2/conv3), :90 (dynamics) and the 1x1 head convs of :81, :100, :102.
+#pragma once
+#include "mzgo_common.hpp"
+
+#ifndef MZGO_WINO_SYNC
+#define MZGO_WINO_SYNC 0
+#endif
+#ifndef MZGO_WINO_PF
+#define MZGO_WINO_PF 8
+#endif
+#ifndef MZGO_WINO_PINB
+#define MZGO_WINO_PINB 1
+#endif
+#ifndef MZGO_WINO_XG
+#define MZGO_WINO_XG 2
+#endif
+
+namespace mzgo {
+constexpr int kWinoXG = MZGO_WINO_XG;   // xi per accumulation group (A stream order, pack_wino)
+}
+
+namespace mzgo {
+
+template <class G>
+struct Wino {
+  static constexpr int TY = (G::N + 1) / 2;   // F(2,3) tiles along rows
+  static constexpr int TX = (G::N + 2) / 3;   // F(3,3) tiles along columns
+  static constexpr int T = TY * TX;           // tiles (MFMA columns)
+  static constexpr int XI = 20;               // 4 x 5 transform points
+  static_assert(T <= 16, "tiles must fit one MFMA column tile");
+  // V floats for CIN input channels: [xi][h][s4][kq][t16][e4]
+  template <int CIN>
+  static constexpr int v_floats() { return XI * CIN * 16; }
+  // exchange buffer [m][h][ox*4 + r][lane] + head partials [m][3][CS]
+  template <int COUT>
+  static constexpr int red_floats() { return (COUT / 16) * 2 * 12 * 64; }
+};
+
+// Transform one board into V.  src: [cin][src_stride] (global, f32); emb:
+// per-channel value added at on-board cells (the action-embedding
+// broadcast-add of self_play.py:87-89) or null.  Channel c = h*CH +
+// 4*(4*s4 + e) + kq is stored at V[((((xi*2 + h)*S4 + s4)*4 + kq)*16 + t)*4 + e]
+// so a lane's B operand for 4 consecutive k-steps is one ds_read_b128.
+// The board is fetched once with coalesced loads (both cin halves in flight)
+// and staged one half at a time through raw ([CH][RAW_STRIDE], LDS).  Cell
+// N*N of each raw row is 0 (pooled latents keep 0 in their pad cells).
+// All threads; returns synchronised.
+template <class G>
+struct WinoRaw {
+  static constexpr int STRIDE = G::CS + (36 - G::CS % 32) % 32;  // >= CS, == 4 mod 32
+  static constexpr int CH_MAX = G::CINMAX / 2;
+};
+
+template <class G, int CIN>
+__device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restrict__ raw,
+                                           const float* __restrict__ src, int src_stride,
+                                           const float* __restrict__ emb, Stamp* st = nullptr) {
+  typedef Wino<G> W;
+  constexpr int CH = CIN / 2, S4 = CH / 16, RS = WinoRaw<G>::STRIDE;
+  static_assert(CIN % 32 == 0, "two cin halves of whole 4-k-step groups");
+  constexpr int ITEMS = S4 * 4;               // (s4, kq) wave items of one half, 64 (t, e) lanes each
+  constexpr int Q = G::CS / 4;                // float4 per pooled channel row
+  constexpr int NQ = CH * Q;                  // float4 per half
+  constexpr int PER = (NQ + G::THREADS - 1) / G::THREADS;
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+  const int t = lane & 15, e = lane >> 4;
+  const int ty = t / W::TX, tx = t - ty * W::TX;
+  const bool tile = t < W::T;
+  const bool pooled = src_stride == G::CS;
+
+  // both halves' rows in flight at once (pooled layout: 16-byte loads)
+  float4 rg[2][PER];
+  float eg[2][(ITEMS + G::WAVES - 1) / G::WAVES];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int k = 0; k < (ITEMS + G::WAVES - 1) / G::WAVES; ++k) {
+      const int it = wave + k * G::WAVES;
+      const int cl = 4 * (4 * (it / 4) + e) + it % 4;
+      eg[hh][k] = (emb && it < ITEMS) ? emb[hh * CH + cl] : 0.f;
+    }
+  if (pooled) {
+    const float4* s4p = reinterpret_cast<const float4*>(src);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int i = threadIdx.x + p * G::THREADS;
+        rg[hh][p] = i < NQ ? s4p[hh * NQ + i] : float4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();                   // raw is free again
+    if (pooled) {
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int i = threadIdx.x + p * G::THREADS;
+        if (i < NQ) {
+          const int cl = i / Q, q = i - cl * Q;
+          *reinterpret_cast<float4*>(raw + cl * RS + q * 4) = rg[h][p];
+        }
+      }
+    } else {
+      for (int i = threadIdx.x; i < CH * (G::CELLS + 1); i += G::THREADS) {
+        const int cl = i / (G::CELLS + 1), j = i - cl * (G::CELLS + 1);
+        raw[cl * RS + j] = j < G::CELLS ? src[(size_t)(h * CH + cl) * src_stride + j] : 0.f;  // + zero slot
+      }
+    }
+    __syncthreads();
+    if (st) st->lap(20 + h);
+#pragma unroll
+    for (int k = 0; k < (ITEMS + G::WAVES - 1) / G::WAVES; ++k) {
+      const int it = wave + k * G::WAVES;
+      if (it >= ITEMS) break;
+      const int s4 = it / 4, kq = it % 4;
+      const int cl = 4 * (4 * s4 + e) + kq;
+      const float ec = eg[h][k];
+      const float* s = raw + cl * RS;
+      float d[4][5];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 5; ++b) {
+          // every lane reads (off-board taps read the zero slot, cell N*N):
+          // no exec-masked LDS reads, each waited for on its own
+          const int y = 2 * ty - 1 + a, x = 3 * tx - 1 + b;
+          const bool ok = tile && y >= 0 && y < G::N && x >= 0 && x < G::N;
+          const float v = s[ok ? y * G::N + x : G::CELLS];
+          d[a][b] = ok ? v + ec : 0.f;
+        }
+      float u[4][5];
+#pragma unroll
+      for (int b = 0; b < 5; ++b) {           // BT2 along rows
+        u[0][b] = d[0][b] - d[2][b];
+        u[1][b] = d[1][b] + d[2][b];
+        u[2][b] = d[2][b] - d[1][b];
+        u[3][b] = d[3][b] - d[1][b];
+      }
+      float* vb = V + ((size_t)(h * S4 + s4) * 4 + kq) * 64 + t * 4 + e;
+      constexpr int XSTRIDE = 2 * S4 * 4 * 64;  // floats between xi planes
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {           // BT3 along columns
+        const float* q = u[i];
+        vb[(i * 5 + 0) * XSTRIDE] = ((2.f * q[0] + q[1]) - 2.f * q[2]) - q[3];
+        vb[(i * 5 + 1) * XSTRIDE] = (2.f * q[1] + 3.f * q[2]) + q[3];
+        vb[(i * 5 + 2) * XSTRIDE] = (q[2] - 2.f * q[1]) + q[3];
+        vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
+        vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// AT2 (2 x 4) and AT3 (3 x 5) of the output transform
+__device__ __forceinline__ constexpr float wino_at2(int oy, int i) {
+  return oy == 0 ? (i < 3 ? 1.f : 0.f) : (i == 0 ? 0.f : (i == 2 ? -1.f : 1.f));
+}
+__device__ __forceinline__ constexpr float wino_at3(int ox, int j) {
+  return ox == 0 ? (j < 4 ? 1.f : 0.f)
+                 : (ox == 1 ? (j == 0 ? 0.f : (j == 1 ? 1.f : (j == 2 ? -1.f : (j == 3 ? -2.f : 0.f))))
+                            : (j == 0 ? 0.f : (j == 3 ? 4.f : 1.f)));
+}
+
+// GEMMs + output transform + bias/ReLU + store + fused 1x1 heads.
+// V: transformed input (LDS, wino_input); red: exchange buffer (LDS, may
+// alias V); hp: head partials [COUT/16][3][CS] (LDS, disjoint from red).
+// upk: U packed [m][h][pos][lane][4], pos = ((xl/XG)*KP + k)*XG + xl%XG for
+// xi = h*10 + xl and k-position k (pack_wino).  out: [COUT][out_stride]
+// global; cells >= out_cells are not stored.  Returns synchronised.
+template <class G, int CIN, int COUT, int NH>
+__device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, const float* __restrict__ upk,
+                                          const float* __restrict__ bias, float* __restrict__ out,
+                                          int out_stride, int out_cells, const float* __restrict__ head_w,
+                                          Stamp* st = nullptr) {
+  typedef Wino<G> W;
+  constexpr int CH = CIN / 2, S4 = CH / 16, MT = COUT / 16, XI = W::XI;
+  constexpr int XH = XI / 2;                  // xi per wave (two xi halves)
+  constexpr int KP = CIN / 16;                // float4 k-positions per xi (4 k-steps each)
+  constexpr int L = XH * KP;                  // float4 A loads (and B reads) per wave
+  constexpr int PF = MZGO_WINO_PF;             // A prefetch depth (float4 registers)
+  static_assert(2 * MT <= G::WAVES, "one wave per (cout tile, xi half)");
+  constexpr int XG = kWinoXG;
+  static_assert(XH % XG == 0, "xi groups");
+  const int lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+  const int m = wave >> 1, h = wave & 1;
+  const bool active = wave < 2 * MT;
+  const int kq = lane >> 4, t = lane & 15;
+
+  f32x4 yp[6];                                // Y partial [oy*3 + ox], component r = cout row
+#pragma unroll
+  for (int o = 0; o < 6; ++o) yp[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const unsigned long long t_loop = st ? __builtin_amdgcn_s_memtime() : 0ull;
+  if (active) {
+    // this wave: xi in [h*XH, h*XH + XH), all CIN (KP float4 k-positions per xi).
+    // A stream: positions pos = ((g*KP + k)*XG + q) for local xi g*XG + q, in
+    // consumption order (pack_wino), PF float4 registers ahead
+    const f32x4* ap = reinterpret_cast<const f32x4*>(upk) + (size_t)(m * 2 + h) * L * 64 + lane;
+    const f32x4* bp = reinterpret_cast<const f32x4*>(V) + (size_t)h * XH * KP * 64 + lane;
+    auto bidx = [&](int xl, int k) { return (xl * KP + k) * 64; };
+    f32x4 ar[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ar[p] = ap[p * 64];
+    f32x4 bn[XG];
+#pragma unroll
+    for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(q, 0)];
+#pragma unroll
+    for (int g = 0; g < XH / XG; ++g) {       // XG independent accumulation chains
+#if MZGO_WINO_SYNC > 0
+      // pacing barrier: keeps the SIMD's waves in step (oldest-first issue
+      // otherwise leaves the youngest wave to finish alone)
+      if constexpr (2 * MT == G::WAVES)
+        if (g > 0 && g % MZGO_WINO_SYNC == 0) __builtin_amdgcn_s_barrier();
+#endif
+      f32x4 acc[XG];
+#pragma unroll
+      for (int q = 0; q < XG; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const int pos0 = (g * KP + k) * XG;
+        f32x4 a[XG], b[XG];
+#pragma unroll
+        for (int q = 0; q < XG; ++q) { a[q] = ar[(pos0 + q) % PF]; b[q] = bn[q]; }
+#ifndef MZGO_DIAG_NOB
+        // next B operands
+        if (k + 1 < KP) {
+#pragma unroll
+          for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(g * XG + q, k + 1)];
+        } else if (g + 1 < XH / XG) {
+#pragma unroll
+          for (int q = 0; q < XG; ++q) bn[q] = bp[bidx((g + 1) * XG + q, 0)];
+        }
+#endif
+#if MZGO_WINO_PINB
+        __builtin_amdgcn_sched_barrier(0);      // issue the next B reads before these MFMAs
+#endif
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int q = 0; q < XG; ++q)
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][e], b[q][e], acc[q], 0, 0, 0);
+#ifndef MZGO_DIAG_NOA
+#pragma unroll
+        for (int q = 0; q < XG; ++q)
+          if (pos0 + q + PF < L) ar[(pos0 + q) % PF] = ap[(pos0 + q + PF) * 64];
+#endif
+        // keep the refill loads here: left alone, the scheduler sinks them
+        // next to their use (to save VGPRs) and exposes the L2 latency
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // fold M_xi into the output-tile partials: Y[oy][ox] += AT2[oy][i] AT3[ox][j] M
+#pragma unroll
+      for (int q = 0; q < XG; ++q) {
+        const int xl = g * XG + q;
+        const f32x4 mv = acc[q];
+#pragma unroll
+        for (int oy = 0; oy < 2; ++oy)
+#pragma unroll
+          for (int ox = 0; ox < 3; ++ox) {
+            // xi = h*XH + xl: i = xi / 5, j = xi % 5 (h is wave-uniform; both
+            // halves are expanded at compile time and selected)
+            const float c0 = wino_at2(oy, xl / 5) * wino_at3(ox, xl % 5);
+            const float c1 = wino_at2(oy, (XH + xl) / 5) * wino_at3(ox, (XH + xl) % 5);
+            if (h == 0) {
+              if (c0 == 1.f) yp[oy * 3 + ox] += mv;
+              else if (c0 == -1.f) yp[oy * 3 + ox] -= mv;
+              else if (c0 != 0.f) yp[oy * 3 + ox] += c0 * mv;
+            } else {
+              if (c1 == 1.f) yp[oy * 3 + ox] += mv;
+              else if (c1 == -1.f) yp[oy * 3 + ox] -= mv;
+              else if (c1 != 0.f) yp[oy * 3 + ox] += c1 * mv;
+            }
+          }
+      }
+    }
+  }
+  if (st) { st->wave_add(8 + wave, __builtin_amdgcn_s_memtime() - t_loop); st->lap(6); }
+
+  // epilogue constants before any store (see conv3x3_ring)
+  float bb[4], hw[NH > 0 ? NH : 1][4];
+  if (active) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = m * 16 + kq * 4 + r;
+      bb[r] = bias[co];
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh) hw[hh][r] = head_w[hh * COUT + co];
+    }
+  }
+  __syncthreads();                            // V is dead: red may overwrite it
+  // wave (m, h) hands its partial of output row oy = 1 - h to its partner
+  // (the other xi half of the same cout tile)
+  if (active) {
+#pragma unroll
+    for (int ox = 0; ox < 3; ++ox)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[((m * 2 + h) * 12 + ox * 4 + r) * 64 + lane] = yp[(1 - h) * 3 + ox][r];
+  }
+  __syncthreads();
+  if (st) st->lap(7);
+  if (active) {
+    const int oy = h;
+    const int ty = t / W::TX, tx = t - ty * W::TX;
+    const int y = 2 * ty + oy;
+    float hsum[NH > 0 ? NH : 1][3];
+#pragma unroll
+    for (int hh = 0; hh < (NH > 0 ? NH : 1); ++hh)
+#pragma unroll
+      for (int ox = 0; ox < 3; ++ox) hsum[hh][ox] = 0.f;
+#pragma unroll
+    for (int ox = 0; ox < 3; ++ox) {
+      const int x = 3 * tx + ox;
+      const bool valid = t < W::T && y < G::N && x < G::N;
+      const int cell = y * G::N + x;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float other = red[((m * 2 + (1 - h)) * 12 + ox * 4 + r) * 64 + lane];
+        const float mine = yp[oy * 3 + ox][r];
+        // fixed order: (xi half 0) + (xi half 1)
+        float v = (h == 0 ? mine + other : other + mine) + bb[r];
+        v = v > 0.f ? v : 0.f;
+        v = valid ? v : 0.f;
+        const int co = m * 16 + kq * 4 + r;
+        // streaming store: the latent is read back (from HBM) only when the
+        // node is expanded, so keep it from evicting the U stream from L2
+        if (out != nullptr && valid && cell < out_cells)
+          __builtin_nontemporal_store(v, out + (size_t)co * out_stride + cell);
+#pragma unroll
+        for (int hh = 0; hh < NH; ++hh) hsum[hh][ox] = __builtin_fmaf(hw[hh][r], v, hsum[hh][ox]);
+      }
+    }
+    if constexpr (NH > 0) {
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh)
+#pragma unroll
+        for (int ox = 0; ox < 3; ++ox) {
+          float v = hsum[hh][ox];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int x = 3 * tx + ox;
+          if (kq == 0 && t < W::T && y < G::N && x < G::N) hp[(m * 3 + hh) * G::CS + y * G::N + x] = v;
+        }
+    }
+  }
+  __syncthreads();
+}
+
+}  // namespace mzgo

@@ -73,18 +73,21 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 8), np.uint64)
+    buf = np.zeros((G, 24), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
     ms = timeit(lambda: seng.search(obs), reps=1)
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))
-    names = ["select", "stage", "conv_epilogue", "heads", "priors", "backup", "conv_loop", "conv_sync"]
-    per_sim = buf.astype(np.float64).mean(0) / (2 * S)            # warm-up call inside timeit + 1 rep
+    names = ["select", "stage", "conv_epilogue", "heads_backup", "p4", "p5", "conv_loop", "conv_sync"]
+    allp = buf.astype(np.float64).mean(0) / (2 * S)               # warm-up call inside timeit + 1 rep
+    per_sim, waves = allp[:8], allp[8:20]
     total = per_sim.sum()
     print(json.dumps({"N": N, "G": G, "S": S, "search_ms": ms,
                       "cycles_per_sim": {n: round(float(v)) for n, v in zip(names, per_sim) },
                       "share": {n: round(float(v / total), 3) for n, v in zip(names, per_sim)},
+                      "wave_conv_loop": [round(float(v)) for v in waves if v > 0],
+                      "stage_split": [round(float(v)) for v in allp[20:24]],
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 
