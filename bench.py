@@ -42,6 +42,25 @@ def algorithmic_flops(N, C, S):
     return sim, root
 
 
+def executed_mfma_flops(N, C, S):
+    """MFMA FLOPs the kernel actually issues per move (16x16x4 f32: 2048 each).
+
+    9x9 runs its latent convs as Winograd F(2,3)xF(3,3) GEMMs (mzgo_wino.hpp):
+    20 transform points x (COUT/16) cout tiles x (CIN/4) k-steps, one 16-column
+    tile of 15 board tiles.  Other boards: the direct implicit GEMM over
+    16-cell column tiles.  conv1 (6 -> 64, cin padded to 8) is always direct.
+    """
+    ct = (N * N + 15) // 16
+    conv1 = 9 * 2 * (64 // 16) * ct
+    if N == 9:
+        wino = lambda cin, cout: 20 * (cout // 16) * (cin // 4)
+        dyn, rep = wino(C, C), wino(64, 64) + wino(64, C)
+    else:
+        direct = lambda cin, cout: 9 * (cin // 4) * (cout // 16) * ct
+        dyn, rep = direct(C, C), direct(64, 64) + direct(64, C)
+    return 2048 * (S * dyn + conv1 + rep)
+
+
 def cpu_baseline(N, C, S, budget_s=12.0):
     """The oracle (CPU restatement of self_play.py's MCTS, batch-1 torch net,
     object tree) timed on this host with one thread, on a bounded sample."""
@@ -163,6 +182,7 @@ def main():
         per_launch_moves = moves / world / args.steps
         launch_flops = per_launch_moves * (S * sim_f + root_f)
         achieved = launch_flops / avg_kern_s / 1e12
+        mfma_exec = per_launch_moves * executed_mfma_flops(N, C, S) / avg_kern_s / 1e12
         peak = 157.3
         out = {
             "metric": "MCTS simulations/sec (whole node) + self-play moves/sec, 9x9 Go, 200 sims/move",
@@ -183,7 +203,11 @@ def main():
                        "parallelism": f"game-sharded x{world}", "compat": "reference"},
             "roofline": {"bound": "mfma", "kernel": "k_selfplay_move", "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                         "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3},
+                         "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3,
+                         # what the MFMA pipes actually execute (Winograd on 9x9 issues
+                         # fewer MFMA FLOPs than the direct conv's algorithmic count)
+                         "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak,
+                         "algorithm": "winograd F(2,3)xF(3,3)" if N == 9 else "direct implicit GEMM"},
         }
         prof = os.path.join(ROOT, "profiles", "latest_summary.json")
         if os.path.exists(prof):

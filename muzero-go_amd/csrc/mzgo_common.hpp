@@ -75,17 +75,31 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // ---------------------------------------------------------------------------
 constexpr int kStampPhases = 24;   // 0-7 phases (thread 0), 8-19 per-wave conv loops
 #ifdef MZGO_STAMPS
+// Phase sums accumulate in LDS (a global read-modify-write per lap would put
+// an HBM round trip on the measured wave's critical path); flush() adds them
+// to the global buffer once.
 struct Stamp {
   unsigned long long* buf;
+  unsigned long long* lds;
   unsigned long long t;
-  __device__ explicit Stamp(unsigned long long* b) : buf(b) { t = __builtin_amdgcn_s_memtime(); }
+  __device__ explicit Stamp(unsigned long long* b) : buf(b) {
+    __shared__ unsigned long long stamp_lds[kStampPhases];
+    lds = stamp_lds;
+    if (threadIdx.x < kStampPhases) lds[threadIdx.x] = 0;
+    __syncthreads();
+    t = __builtin_amdgcn_s_memtime();
+  }
   __device__ void lap(int phase) {
     unsigned long long now = __builtin_amdgcn_s_memtime();
-    if (buf && threadIdx.x == 0) buf[blockIdx.x * kStampPhases + phase] += now - t;
+    if (threadIdx.x == 0) lds[phase] += now - t;
     t = now;
   }
   __device__ void wave_add(int phase, unsigned long long cycles) {
-    if (buf && (threadIdx.x & 63) == 0) buf[blockIdx.x * kStampPhases + phase] += cycles;
+    if ((threadIdx.x & 63) == 0) lds[phase] += cycles;   // one slot per wave
+  }
+  __device__ void flush() {
+    __syncthreads();
+    if (buf && threadIdx.x < kStampPhases) buf[blockIdx.x * kStampPhases + threadIdx.x] += lds[threadIdx.x];
   }
 };
 #else
@@ -93,6 +107,7 @@ struct Stamp {
   __device__ explicit Stamp(unsigned long long*) {}
   __device__ void lap(int) {}
   __device__ void wave_add(int, unsigned long long) {}
+  __device__ void flush() {}
 };
 #endif
 
@@ -108,23 +123,103 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// Cross-lane moves by DPP (no LDS round trip, unlike ds_bpermute): quad_perm
+// xor-1 / xor-2 and row_ror 4 / 8 combine the 16 lanes of a row; the four row
+// results are then read with v_readlane.  Valid for order-insensitive
+// reductions (min, max, argmax) with all 64 lanes active.
+namespace dpp {
+enum : int { XOR1 = 0xB1, XOR2 = 0x4E, ROR4 = 0x124, ROR8 = 0x128 };
+template <int C>
+__device__ __forceinline__ int mov(int v) { return __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, false); }
+template <int C>
+__device__ __forceinline__ float mov(float v) { return __int_as_float(mov<C>(__float_as_int(v))); }
+template <int C>
+__device__ __forceinline__ double mov(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = mov<C>((int)x), hi = mov<C>((int)(x >> 32));
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ int lane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float lane(float v, int l) { return __int_as_float(lane(__float_as_int(v), l)); }
+__device__ __forceinline__ double lane(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = lane((int)x, l), hi = lane((int)(x >> 32), l);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+}  // namespace dpp
+
+// op must be commutative and associative on the values involved (min, max)
+template <typename T, class Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+  v = op(v, dpp::mov<dpp::XOR1>(v));
+  v = op(v, dpp::mov<dpp::XOR2>(v));
+  v = op(v, dpp::mov<dpp::ROR4>(v));
+  v = op(v, dpp::mov<dpp::ROR8>(v));
+  return op(op(dpp::lane(v, 0), dpp::lane(v, 16)), op(dpp::lane(v, 32), dpp::lane(v, 48)));
 }
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o); v = w > v ? w : v; }
-  return v;
+  return wave_reduce(v, [](T a, T b) { return b > a ? b : a; });
 }
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o); v = w < v ? w : v; }
+  return wave_reduce(v, [](T a, T b) { return b < a ? b : a; });
+}
+
+// v[i] + v[i ^ 32] and v[i] + v[i ^ 16] via the gfx950 permlane swaps
+// (each returns both halves; addition is commutative, so the sum is the
+// butterfly's exactly)
+__device__ __forceinline__ unsigned bits_of(float v) { return __float_as_uint(v); }
+__device__ __forceinline__ float from_bits(unsigned v, float) { return __uint_as_float(v); }
+template <bool SWAP32>
+__device__ __forceinline__ float swap_add(float v) {
+  const auto r = SWAP32 ? __builtin_amdgcn_permlane32_swap(bits_of(v), bits_of(v), false, false)
+                        : __builtin_amdgcn_permlane16_swap(bits_of(v), bits_of(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <bool SWAP32>
+__device__ __forceinline__ double swap_add(double v) {
+  const long long x = __double_as_longlong(v);
+  const unsigned lo = (unsigned)x, hi = (unsigned)(x >> 32);
+  const auto rl = SWAP32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                         : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = SWAP32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                         : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double a = __longlong_as_double((long long)rl[0] | ((long long)rh[0] << 32));
+  const double b = __longlong_as_double((long long)rl[1] | ((long long)rh[1] << 32));
+  return a + b;
+}
+
+// Butterfly sum (xor 32, 16, 8, 4, 2, 1) without LDS traffic: permlane swaps
+// for 32/16, DPP inside a row for the rest (row_ror 8 == xor 8; after it the
+// row is 8-periodic, so row_ror 4 acts as xor 4).  Bit-identical to the
+// __shfl_xor butterfly.  All 64 lanes active.
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  v = swap_add<true>(v);
+  v = swap_add<false>(v);
+  v = v + dpp::mov<dpp::ROR8>(v);
+  v = v + dpp::mov<dpp::ROR4>(v);
+  v = v + dpp::mov<dpp::XOR2>(v);
+  v = v + dpp::mov<dpp::XOR1>(v);
   return v;
+}
+// (score, action, payload) argmax, ties to the lower action; all lanes get it
+__device__ __forceinline__ void wave_argmax(double& s, int& a, int& c) {
+  auto step = [&](double os, int oa, int oc) {
+    if (os > s || (os == s && oa < a)) { s = os; a = oa; c = oc; }
+  };
+  step(dpp::mov<dpp::XOR1>(s), dpp::mov<dpp::XOR1>(a), dpp::mov<dpp::XOR1>(c));
+  step(dpp::mov<dpp::XOR2>(s), dpp::mov<dpp::XOR2>(a), dpp::mov<dpp::XOR2>(c));
+  step(dpp::mov<dpp::ROR4>(s), dpp::mov<dpp::ROR4>(a), dpp::mov<dpp::ROR4>(c));
+  step(dpp::mov<dpp::ROR8>(s), dpp::mov<dpp::ROR8>(a), dpp::mov<dpp::ROR8>(c));
+  double rs[4];
+  int ra[4], rc[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { rs[r] = dpp::lane(s, 16 * r); ra[r] = dpp::lane(a, 16 * r); rc[r] = dpp::lane(c, 16 * r); }
+  s = rs[0]; a = ra[0]; c = rc[0];
+#pragma unroll
+  for (int r = 1; r < 4; ++r) step(rs[r], ra[r], rc[r]);
 }
 
 // ---------------------------------------------------------------------------
@@ -146,8 +241,8 @@ __device__ __forceinline__ T np_pairwise_sum(const T* x) {
     const int j = lane_id() & 7;
     T r = x[j];
     for (int i = 8; i < STOP; i += 8) r = r + x[i + j];
-    T r0 = __shfl(r, 0), r1 = __shfl(r, 1), r2 = __shfl(r, 2), r3 = __shfl(r, 3);
-    T r4 = __shfl(r, 4), r5 = __shfl(r, 5), r6 = __shfl(r, 6), r7 = __shfl(r, 7);
+    T r0 = dpp::lane(r, 0), r1 = dpp::lane(r, 1), r2 = dpp::lane(r, 2), r3 = dpp::lane(r, 3);
+    T r4 = dpp::lane(r, 4), r5 = dpp::lane(r, 5), r6 = dpp::lane(r, 6), r7 = dpp::lane(r, 7);
     T res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
 #pragma unroll
     for (int i = STOP; i < N; ++i) res = res + x[i];

@@ -97,6 +97,7 @@ struct Smem<G, true> {
     struct {
       float red[Wino<G>::template red_floats<G::C>()];
       float hp[(G::C / 16) * 3 * G::CS];
+      alignas(16) float outs[G::C * G::CS];           // conv output staging
     } x;
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
   } u;
@@ -122,7 +123,8 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
   if constexpr (G::WINO) {
     wino_input<G, CIN>(sm.u.v, sm.raw, src, src_stride, emb, st);
     if (st) st->lap(1);
-    wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, w, b, dst, dst_stride, out_cells, head_w, st);
+    wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, w, b, dst, dst_stride, out_cells,
+                                head_w, st);
   } else {
     stage_board<G>(sm.u.in, src, src_stride, CIN, emb);
     __syncthreads();
@@ -161,6 +163,7 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
   conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
   __syncthreads();
   latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, lat, lat_stride, oc, nullptr);
+  __syncthreads();                                         // conv2's stores before conv3 reads them
   latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, lat, lat_stride, nullptr, lat, lat_stride, oc,
                               np.head_w + G::C);
   if (wave_id() == 0)
@@ -240,7 +243,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
   Stamp st(E.stamps);
   for (int sim = 0; sim < S; ++sim) {
     if (wave_id() == 0) {
-      const int a = select_leaf<G>(sm.t, T, sp, key, sim);
+      const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st);
       if (lane_id() == 0) sm.t.action = a;
     }
     __syncthreads();
@@ -276,6 +279,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
     st.lap(3);
   }
   __syncthreads();
+  st.flush();
   tree_flush<G>(T, nodes);
   if (threadIdx.x == 0) E.nodes[g] = nodes;
   __syncthreads();

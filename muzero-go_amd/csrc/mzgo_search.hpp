@@ -359,7 +359,7 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 // ---------------------------------------------------------------------------
 template <class G>
 __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, const SearchParams& sp,
-                                  uint64_t key, int sim) {
+                                  uint64_t key, int sim, Stamp* st = nullptr) {
   const int lane = lane_id();
   int node = 0, depth = 0;
   for (int guard = 0; guard <= sp.num_simulations + 1; ++guard) {
@@ -446,17 +446,12 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
         if (sc > best_s || (sc == best_s && a < best_a)) { best_s = sc; best_a = a; best_c = ch[j]; }
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double os = __shfl_xor(best_s, o);
-      const int oa = __shfl_xor(best_a, o);
-      const int oc = __shfl_xor(best_c, o);
-      if (os > best_s || (os == best_s && oa < best_a)) { best_s = os; best_a = oa; best_c = oc; }
-    }
+    wave_argmax(best_s, best_a, best_c);
     if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return -1; }
     depth += 1;
     if (lane == 0) T.path_[depth] = best_c;
     node = best_c;
+    if (st) st->lap(depth == 1 ? 22 : 23);
   }
   t.leaf = node;
   t.depth = depth;

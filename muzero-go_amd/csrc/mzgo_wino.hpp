@@ -30,6 +30,9 @@
 #ifndef MZGO_WINO_PF
 #define MZGO_WINO_PF 8
 #endif
+#ifndef MZGO_NT_STORE
+#define MZGO_NT_STORE 1   // whole-row streaming stores of node latents
+#endif
 #ifndef MZGO_WINO_PINB
 #define MZGO_WINO_PINB 1
 #endif
@@ -187,12 +190,16 @@ __device__ __forceinline__ constexpr float wino_at3(int ox, int j) {
 
 // GEMMs + output transform + bias/ReLU + store + fused 1x1 heads.
 // V: transformed input (LDS, wino_input); red: exchange buffer (LDS, may
-// alias V); hp: head partials [COUT/16][3][CS] (LDS, disjoint from red).
+// alias V); hp: head partials [COUT/16][3][CS]; outs: output staging
+// [COUT][CS] (LDS; red, hp and outs disjoint).  hp is complete on return;
+// the stores to ``out`` are issued but not synchronised.
 // upk: U packed [m][h][pos][lane][4], pos = ((xl/XG)*KP + k)*XG + xl%XG for
 // xi = h*10 + xl and k-position k (pack_wino).  out: [COUT][out_stride]
-// global; cells >= out_cells are not stored.  Returns synchronised.
+// global; cells >= out_cells are not stored (pooled rows, stride == out_cells
+// == CS, are stored whole with their zero pad cells).
 template <class G, int CIN, int COUT, int NH>
-__device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, const float* __restrict__ upk,
+__device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, float* outs,
+                                          const float* __restrict__ upk,
                                           const float* __restrict__ bias, float* __restrict__ out,
                                           int out_stride, int out_cells, const float* __restrict__ head_w,
                                           Stamp* st = nullptr) {
@@ -347,10 +354,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         v = v > 0.f ? v : 0.f;
         v = valid ? v : 0.f;
         const int co = m * 16 + kq * 4 + r;
-        // streaming store: the latent is read back (from HBM) only when the
-        // node is expanded, so keep it from evicting the U stream from L2
-        if (out != nullptr && valid && cell < out_cells)
-          __builtin_nontemporal_store(v, out + (size_t)co * out_stride + cell);
+        if (valid) outs[co * G::CS + cell] = v;      // staged for a coalesced store
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) hsum[hh][ox] = __builtin_fmaf(hw[hh][r], v, hsum[hh][ox]);
       }
@@ -361,14 +365,39 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
 #pragma unroll
         for (int ox = 0; ox < 3; ++ox) {
           float v = hsum[hh][ox];
-          v += __shfl_xor(v, 16);
-          v += __shfl_xor(v, 32);
+          v = swap_add<false>(v);               // + lane ^ 16
+          v = swap_add<true>(v);                // + lane ^ 32
           const int x = 3 * tx + ox;
           if (kq == 0 && t < W::T && y < G::N && x < G::N) hp[(m * 3 + hh) * G::CS + y * G::N + x] = v;
         }
     }
   }
+  // pad cells of the staged rows are 0 (the pooled layout keeps them 0)
+  for (int i = threadIdx.x; i < COUT * (G::CS - G::CELLS); i += G::THREADS) {
+    const int co = i / (G::CS - G::CELLS);
+    outs[co * G::CS + G::CELLS + (i - co * (G::CS - G::CELLS))] = 0.f;
+  }
   __syncthreads();
+  // whole-row stores (the tile-ordered epilogue would scatter 4-byte writes)
+  if (out != nullptr) {
+    if (out_stride == G::CS && out_cells == G::CS) {
+      constexpr int Q = G::CS / 4;
+      for (int i = threadIdx.x; i < COUT * Q; i += G::THREADS) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(outs + i * 4);
+#if MZGO_NT_STORE
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out) + i);
+#else
+        reinterpret_cast<f32x4*>(out)[i] = v;
+#endif
+      }
+    } else {
+      for (int i = threadIdx.x; i < COUT * out_cells; i += G::THREADS) {
+        const int co = i / out_cells, j = i - co * out_cells;
+        out[(size_t)co * out_stride + j] = outs[co * G::CS + j];
+      }
+    }
+  }
+  // no barrier: a caller that reads ``out`` back synchronises first
 }
 
 }  // namespace mzgo

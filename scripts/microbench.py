@@ -87,7 +87,8 @@ def stamps_report():
                       "cycles_per_sim": {n: round(float(v)) for n, v in zip(names, per_sim) },
                       "share": {n: round(float(v / total), 3) for n, v in zip(names, per_sim)},
                       "wave_conv_loop": [round(float(v)) for v in waves if v > 0],
-                      "stage_split": [round(float(v)) for v in allp[20:24]],
+                      "stage_split": [round(float(v)) for v in allp[20:22]],
+                      "select_split_root_deeper": [round(float(v)) for v in allp[22:24]],
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 
