@@ -73,7 +73,7 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // scripts/microbench.py).  Thread 0 of each workgroup adds shader-clock
 // deltas per phase into mzgo_stamps[block][phase].
 // ---------------------------------------------------------------------------
-constexpr int kStampPhases = 24;   // 0-7 phases (thread 0), 8-19 per-wave conv loops
+constexpr int kStampPhases = 32;   // 0-7 phases (thread 0), 8-19 per-wave conv loops, 20+ sub-phases
 #ifdef MZGO_STAMPS
 // Phase sums accumulate in LDS (a global read-modify-write per lap would put
 // an HBM round trip on the measured wave's critical path); flush() adds them
@@ -115,6 +115,14 @@ struct Stamp {
 // wave64 helpers
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// lane id that the compiler cannot hoist out of the simulation loop: values
+// derived from it are recomputed (a few VALU ops) instead of being kept live
+// across the whole loop and spilled at 168 VGPRs (3 waves per SIMD)
+__device__ __forceinline__ int lane_id_local() {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 // Order LDS traffic between lanes of one wave (no workgroup barrier needed).

@@ -101,7 +101,7 @@ struct Smem<G, true> {
     } x;
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
   } u;
-  alignas(16) float raw[WinoRaw<G>::CH_MAX * WinoRaw<G>::STRIDE];  // one cin half of the conv input
+  alignas(16) float raw[WinoRaw<G>::FLOATS];              // per-wave staging of conv input rows
   TreeLds<G> t;
   int8_t stone[G::CELLS];
   uint8_t invd[G::CELLS];
@@ -222,21 +222,16 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 // ---------------------------------------------------------------------------
 // One full MCTS.run (self_play.py:148-237) for game slot g.
 // ---------------------------------------------------------------------------
-template <class G, class PlaneFn>
-__device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
-                                  const EngineArrays& E, int g, PlaneFn planes, const double* noise,
-                                  uint64_t key) {
-  const TreeView TV = TreeViewOf<G>::make(E, g);
+// The simulations of one search with the tree accessor Acc (LDS or HBM stats).
+template <class G, class Acc>
+__device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                         const EngineArrays& E, int g, const TreeView& TV, uint64_t key) {
   float* pool = E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS;
   const size_t node_floats = (size_t)G::C * G::CS;
   const int S = sp.num_simulations;
-  TreeAcc<G> T(TV, sm.t, S + 2 <= G::TREE_CAP);
-
-  build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
+  Acc T(TV, sm.t);
   tree_reset_root<G>(T);
   if (threadIdx.x == 0) { sm.t.newest = -1; sm.t.newp_node = -1; }
-  representation<G>(sm, np, planes, pool, G::CS);        // root latent -> node 0
-  if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
   __syncthreads();
 
   int nodes = 1;
@@ -283,6 +278,25 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
   tree_flush<G>(T, nodes);
   if (threadIdx.x == 0) E.nodes[g] = nodes;
   __syncthreads();
+}
+
+template <class G, class PlaneFn>
+__device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                  const EngineArrays& E, int g, PlaneFn planes, const double* noise,
+                                  uint64_t key) {
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
+  representation<G>(sm, np, planes, E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS,
+                    G::CS);                              // root latent -> node 0
+  if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
+  __syncthreads();
+  if constexpr (G::TREE_CAP > 0) {
+    if (sp.num_simulations + 2 <= G::TREE_CAP) {
+      sim_loop<G, TreeAcc<G, true>>(sm, np, sp, E, g, TV, key);
+      return;
+    }
+  }
+  sim_loop<G, TreeAcc<G, false>>(sm, np, sp, E, g, TV, key);
 }
 
 // root-child visit counts and root value of the finished search

@@ -63,38 +63,39 @@ struct TreeLds {
 };
 
 // Tree accessor: node stats, path and the root's child row / priors either in
-// LDS (small boards, S + 2 <= TREE_CAP; copied back to HBM by flush()) or in
-// HBM.  Child rows / priors of non-root nodes always live in HBM.
-template <class G>
+// LDS (L: small boards, S + 2 <= TREE_CAP; copied back to HBM by tree_flush)
+// or in HBM.  Child rows / priors of non-root nodes always live in HBM.  The
+// choice is a template parameter so every access compiles to ds_* or
+// global_* (a runtime pointer choice would make them flat_* accesses).
+template <class G, bool L>
 struct TreeAcc {
+  static_assert(!L || G::TREE_CAP > 0, "LDS tree needs TREE_CAP");
+  static constexpr bool LDS = L;
   TreeView T;
-  int* vis_;
-  double* ws_;
-  int* path_;
-  int* rchild_;       // LDS mirror of the root row, or null
-  double* rprior_;    // LDS mirror of the root priors, or null
-  __device__ __forceinline__ TreeAcc(const TreeView& tv, TreeLds<G>& t, bool lds) : T(tv) {
-    if (G::TREE_CAP > 0 && lds) {
-      vis_ = t.svis; ws_ = t.sws; path_ = t.spath; rchild_ = t.rchild; rprior_ = t.rprior;
-    } else {
-      vis_ = T.visits; ws_ = T.wsum; path_ = T.path; rchild_ = nullptr; rprior_ = nullptr;
-    }
+  TreeLds<G>& t;
+  __device__ __forceinline__ TreeAcc(const TreeView& tv, TreeLds<G>& tl) : T(tv), t(tl) {}
+  __device__ __forceinline__ int vis(int n) const { if constexpr (L) return t.svis[n]; else return T.visits[n]; }
+  __device__ __forceinline__ double ws(int n) const { if constexpr (L) return t.sws[n]; else return T.wsum[n]; }
+  __device__ __forceinline__ void add(int n, double dv) {
+    if constexpr (L) { t.svis[n] += 1; t.sws[n] = t.sws[n] + dv; }
+    else { T.visits[n] += 1; T.wsum[n] = T.wsum[n] + dv; }
   }
-  __device__ __forceinline__ int vis(int n) const { return vis_[n]; }
-  __device__ __forceinline__ double ws(int n) const { return ws_[n]; }
-  __device__ __forceinline__ void add(int n, double dv) { vis_[n] += 1; ws_[n] = ws_[n] + dv; }
-  __device__ __forceinline__ void init(int n) { vis_[n] = 0; ws_[n] = 0.0; }
-  __device__ __forceinline__ int path(int i) const { return path_[i]; }
-  __device__ __forceinline__ void set_path(int i, int n) { path_[i] = n; }
+  __device__ __forceinline__ void init(int n) {
+    if constexpr (L) { t.svis[n] = 0; t.sws[n] = 0.0; } else { T.visits[n] = 0; T.wsum[n] = 0.0; }
+  }
+  __device__ __forceinline__ int path(int i) const { if constexpr (L) return t.spath[i]; else return T.path[i]; }
+  __device__ __forceinline__ void set_path(int i, int n) { if constexpr (L) t.spath[i] = n; else T.path[i] = n; }
   __device__ __forceinline__ int child(int n, int a) const {
-    return (n == 0 && rchild_) ? rchild_[a] : T.child[(size_t)n * G::A + a];
+    if constexpr (L) { if (n == 0) return t.rchild[a]; }
+    return T.child[(size_t)n * G::A + a];
   }
   __device__ __forceinline__ void set_child(int n, int a, int c) {
     T.child[(size_t)n * G::A + a] = c;
-    if (n == 0 && rchild_) rchild_[a] = c;
+    if constexpr (L) { if (n == 0) t.rchild[a] = c; }
   }
-  __device__ __forceinline__ double root_prior(int a) const { return rprior_ ? rprior_[a] : T.root_prior[a]; }
-  __device__ __forceinline__ bool in_lds() const { return rchild_ != nullptr; }
+  __device__ __forceinline__ double root_prior(int a) const {
+    if constexpr (L) return t.rprior[a]; else return T.root_prior[a];
+  }
 };
 
 template <class G>
@@ -120,7 +121,7 @@ __device__ __forceinline__ void build_mask(TreeLds<G>& t, double pass_epsilon, I
 // Wave 0 only.
 template <class G>
 __device__ __forceinline__ void softmax_wave(TreeLds<G>& t) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   float m = -INFINITY;
   for (int a = lane; a < G::A; a += 64) m = fmaxf(m, t.logits[a]);
   m = wave_max(m);
@@ -183,7 +184,7 @@ __device__ __forceinline__ float head_at(const float* hp, int h, int c) {
 template <class G, int NPART>
 __device__ __forceinline__ void heads_value(const float* hp, bool has_reward, const float* hsc, float& reward,
                                             float& value) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   const int hv = has_reward ? 1 : 0;
   const float vb = hsc[HS_VB];
   float vs = 0.f, rs = 0.f;
@@ -213,7 +214,7 @@ __device__ __forceinline__ void heads_value(const float* hp, bool has_reward, co
 // policy logits (cells, then the learned pass logit).  One wave.
 template <class G, int NPART>
 __device__ __forceinline__ void heads_logits(const float* hp, bool has_reward, const float* hsc, float* logits) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   const int hpol = has_reward ? 2 : 1;
   const float pb = hsc[HS_PB];
   for (int c = lane; c < G::CELLS; c += 64) logits[c] = head_at<G, NPART>(hp, hpol, c) + pb;
@@ -233,7 +234,7 @@ __device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward,
 // normalised by numpy's f32 pairwise sum; entries with mask 0 are 0.  Wave 0.
 template <class G>
 __device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst, int node = -1) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   softmax_wave<G>(t);
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
   const float s = np_pairwise_sum<float, G::A>(t.fbuf);
@@ -284,7 +285,7 @@ __device__ __forceinline__ double gamma_draw(uint64_t key, int a, double alpha) 
 template <class G>
 __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
                                    const double* noise, uint64_t key) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   softmax_wave<G>(t);
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
   const float s = np_pairwise_sum<float, G::A>(t.fbuf);
@@ -357,10 +358,10 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 // at t.leaf, or -1 when the walk ends at a terminal node (t.leaf).  The path
 // (node ids, root first) is written to T.path[0..depth].
 // ---------------------------------------------------------------------------
-template <class G>
-__device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, const SearchParams& sp,
+template <class G, class Acc>
+__device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const SearchParams& sp,
                                   uint64_t key, int sim, Stamp* st = nullptr) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   int node = 0, depth = 0;
   for (int guard = 0; guard <= sp.num_simulations + 1; ++guard) {
     const bool root = node == 0;
@@ -379,8 +380,16 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
     for (int j = 0; j < G::AP; ++j) {
       const int a = lane + 64 * j;
       const bool in = a < G::A;
-      P[j] = in ? (root ? T.root_prior(a) : (double)(fresh ? t.newp[a] : pr_row[a])) : 0.0;
-      ch[j] = in ? T.child(node, a) : -1;
+      // three sources, chosen by wave-uniform branches (a select between an LDS
+      // and a global pointer would compile to a flat load)
+      if (root) {
+        asm volatile("" ::: "memory");        // keep the LDS and HBM loads apart (no flat merge)
+        P[j] = in ? T.root_prior(a) : 0.0;
+        ch[j] = in ? T.child(0, a) : -1;
+      } else {
+        P[j] = in ? (fresh ? (double)t.newp[a] : (double)pr_row[a]) : 0.0;
+        ch[j] = in ? T.T.child[(size_t)node * G::A + a] : -1;
+      }
       const bool pos = in && P[j] > 0.0;
       const bool e = pos && mask_of<G>(t, a) > 0.0;
       anypos |= __ballot(pos);
@@ -391,6 +400,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
     uint64_t any_elig = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) any_elig |= elig[j];
+    if (st && root) st->lap(24);
     if ((nvis > 0 && !anypos) || !any_elig) { t.leaf = node; t.depth = depth; return -1; }
 
     if (n_unexp > 0) {
@@ -429,8 +439,10 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
         hi = fmax(hi, q[j]);
       }
     }
+    if (st && root) st->lap(25);
     lo = wave_min(lo);
     hi = wave_max(hi);
+    if (st && root) st->lap(26);
     const double sq = sqrt((double)(nvis > 1 ? nvis : 1));
     double best_s = -INFINITY;
     int best_a = 0x7fffffff, best_c = -1;
@@ -446,10 +458,11 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
         if (sc > best_s || (sc == best_s && a < best_a)) { best_s = sc; best_a = a; best_c = ch[j]; }
       }
     }
+    if (st && root) st->lap(27);
     wave_argmax(best_s, best_a, best_c);
     if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return -1; }
     depth += 1;
-    if (lane == 0) T.path_[depth] = best_c;
+    if (lane == 0) const_cast<Acc&>(T).set_path(depth, best_c);
     node = best_c;
     if (st) st->lap(depth == 1 ? 22 : 23);
   }
@@ -461,9 +474,9 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const TreeAcc<G>& T, c
 // Backup along path[0..depth] (+ the new node nid if >= 0): leaf-most gets
 // +v, alternating sign upward (self_play.py:337-343).  Wave 0; path nodes are
 // distinct, so each lane updates its own node.  Path entry 0 is the root.
-template <class G>
-__device__ __forceinline__ void backup(TreeAcc<G>& T, int depth, int nid, double v) {
-  const int lane = lane_id();
+template <class G, class Acc>
+__device__ __forceinline__ void backup(Acc& T, int depth, int nid, double v) {
+  const int lane = lane_id_local();
   const int off = nid >= 0 ? 1 : 0;
   const int count = depth + 1 + off;              // nodes on the backed-up path
   for (int i = lane; i < count; i += 64) {
@@ -474,19 +487,20 @@ __device__ __forceinline__ void backup(TreeAcc<G>& T, int depth, int nid, double
 }
 
 // Reset a tree to a bare root (children unexpanded, stats zero).  All threads.
-template <class G>
-__device__ __forceinline__ void tree_reset_root(TreeAcc<G>& T) {
+template <class G, class Acc>
+__device__ __forceinline__ void tree_reset_root(Acc& T) {
   for (int a = threadIdx.x; a < G::A; a += G::THREADS) T.set_child(0, a, -1);
   if (threadIdx.x == 0) { T.init(0); T.set_path(0, 0); }
 }
 
 // Write LDS-resident stats of nodes [0, nodes) back to HBM.  All threads.
-template <class G>
-__device__ __forceinline__ void tree_flush(TreeAcc<G>& T, int nodes) {
-  if (!T.in_lds()) return;
-  for (int n = threadIdx.x; n < nodes; n += G::THREADS) {
-    T.T.visits[n] = T.vis_[n];
-    T.T.wsum[n] = T.ws_[n];
+template <class G, class Acc>
+__device__ __forceinline__ void tree_flush(Acc& T, int nodes) {
+  if constexpr (Acc::LDS) {
+    for (int n = threadIdx.x; n < nodes; n += G::THREADS) {
+      T.T.visits[n] = T.t.svis[n];
+      T.T.wsum[n] = T.t.sws[n];
+    }
   }
 }
 

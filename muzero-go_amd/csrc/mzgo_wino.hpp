@@ -66,14 +66,18 @@ struct Wino {
 // broadcast-add of self_play.py:87-89) or null.  Channel c = h*CH +
 // 4*(4*s4 + e) + kq is stored at V[((((xi*2 + h)*S4 + s4)*4 + kq)*16 + t)*4 + e]
 // so a lane's B operand for 4 consecutive k-steps is one ds_read_b128.
-// The board is fetched once with coalesced loads (both cin halves in flight)
-// and staged one half at a time through raw ([CH][RAW_STRIDE], LDS).  Cell
-// N*N of each raw row is 0 (pooled latents keep 0 in their pad cells).
-// All threads; returns synchronised.
+//
+// Work unit: a channel quad (h, s4, kq) = the 4 channels e = 0..3 that share
+// one V row; lane (t, e) transforms tile t of channel e.  Each wave fetches
+// its quads' rows itself (coalesced 16-byte loads, all in flight at once) and
+// stages them in its own slice of raw ([4][RAW_STRIDE] per wave), so the only
+// workgroup barrier is the one before the GEMM.  Cell N*N of each raw row is
+// 0 (pooled latents keep 0 in their pad cells).  All threads; returns
+// synchronised.
 template <class G>
 struct WinoRaw {
   static constexpr int STRIDE = G::CS + (36 - G::CS % 32) % 32;  // >= CS, == 4 mod 32
-  static constexpr int CH_MAX = G::CINMAX / 2;
+  static constexpr int FLOATS = G::WAVES * 4 * STRIDE;             // all waves' slices
 };
 
 template <class G, int CIN>
@@ -83,99 +87,97 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
   typedef Wino<G> W;
   constexpr int CH = CIN / 2, S4 = CH / 16, RS = WinoRaw<G>::STRIDE;
   static_assert(CIN % 32 == 0, "two cin halves of whole 4-k-step groups");
-  constexpr int ITEMS = S4 * 4;               // (s4, kq) wave items of one half, 64 (t, e) lanes each
-  constexpr int Q = G::CS / 4;                // float4 per pooled channel row
-  constexpr int NQ = CH * Q;                  // float4 per half
-  constexpr int PER = (NQ + G::THREADS - 1) / G::THREADS;
-  const int lane = lane_id();
+  constexpr int QUADS = 2 * S4 * 4;           // (h, s4, kq)
+  constexpr int QPW = (QUADS + G::WAVES - 1) / G::WAVES;   // quads per wave
+  constexpr int Q4 = G::CS / 4;               // float4 per pooled channel row
+  constexpr int NQ = 4 * Q4;                  // float4 per quad
+  constexpr int PER = (NQ + 63) / 64;         // float4 loads per lane per quad
+  const int lane = lane_id_local();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   const int t = lane & 15, e = lane >> 4;
   const int ty = t / W::TX, tx = t - ty * W::TX;
   const bool tile = t < W::T;
   const bool pooled = src_stride == G::CS;
+  float* my = raw + wave * 4 * RS;
+  auto chan = [&](int quad, int ee) {         // channel of quad member ee
+    const int h = quad / (S4 * 4), s4 = (quad / 4) % S4, kq = quad % 4;
+    return h * CH + 4 * (4 * s4 + ee) + kq;
+  };
 
-  // both halves' rows in flight at once (pooled layout: 16-byte loads)
-  float4 rg[2][PER];
-  float eg[2][(ITEMS + G::WAVES - 1) / G::WAVES];
+  // all of this wave's rows in flight at once; loads are branch-free
+  // (clamped indices) so the compiler keeps them outstanding together
+  f32x4 rg[QPW][PER];
+  float eg[QPW];
+  const f32x4* s4p = reinterpret_cast<const f32x4*>(src);
+  const float* ebase = emb ? emb : src;
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int k = 0; k < (ITEMS + G::WAVES - 1) / G::WAVES; ++k) {
-      const int it = wave + k * G::WAVES;
-      const int cl = 4 * (4 * (it / 4) + e) + it % 4;
-      eg[hh][k] = (emb && it < ITEMS) ? emb[hh * CH + cl] : 0.f;
-    }
-  if (pooled) {
-    const float4* s4p = reinterpret_cast<const float4*>(src);
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int p = 0; p < PER; ++p) {
-        const int i = threadIdx.x + p * G::THREADS;
-        rg[hh][p] = i < NQ ? s4p[hh * NQ + i] : float4{0.f, 0.f, 0.f, 0.f};
-      }
-  }
-  for (int h = 0; h < 2; ++h) {
-    if (h) __syncthreads();                   // raw is free again
+  for (int k = 0; k < QPW; ++k) {
+    const int quad = min(wave + k * G::WAVES, QUADS - 1);
     if (pooled) {
 #pragma unroll
       for (int p = 0; p < PER; ++p) {
-        const int i = threadIdx.x + p * G::THREADS;
-        if (i < NQ) {
-          const int cl = i / Q, q = i - cl * Q;
-          *reinterpret_cast<float4*>(raw + cl * RS + q * 4) = rg[h][p];
-        }
-      }
-    } else {
-      for (int i = threadIdx.x; i < CH * (G::CELLS + 1); i += G::THREADS) {
-        const int cl = i / (G::CELLS + 1), j = i - cl * (G::CELLS + 1);
-        raw[cl * RS + j] = j < G::CELLS ? src[(size_t)(h * CH + cl) * src_stride + j] : 0.f;  // + zero slot
+        const int i = min(lane + 64 * p, NQ - 1);
+        rg[k][p] = s4p[chan(quad, i / Q4) * Q4 + i % Q4];
       }
     }
-    __syncthreads();
-    if (st) st->lap(20 + h);
+    eg[k] = ebase[chan(quad, e)];
+  }
+  if (st) st->lap(20);
+
 #pragma unroll
-    for (int k = 0; k < (ITEMS + G::WAVES - 1) / G::WAVES; ++k) {
-      const int it = wave + k * G::WAVES;
-      if (it >= ITEMS) break;
-      const int s4 = it / 4, kq = it % 4;
-      const int cl = 4 * (4 * s4 + e) + kq;
-      const float ec = eg[h][k];
-      const float* s = raw + cl * RS;
-      float d[4][5];
+  for (int k = 0; k < QPW; ++k) {
+    const int quad = wave + k * G::WAVES;
+    if (quad >= QUADS) break;                 // wave-uniform
+    if (k) wave_lds_sync();                   // previous quad's reads are done
+    if (pooled) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 5; ++b) {
-          // every lane reads (off-board taps read the zero slot, cell N*N):
-          // no exec-masked LDS reads, each waited for on its own
-          const int y = 2 * ty - 1 + a, x = 3 * tx - 1 + b;
-          const bool ok = tile && y >= 0 && y < G::N && x >= 0 && x < G::N;
-          const float v = s[ok ? y * G::N + x : G::CELLS];
-          d[a][b] = ok ? v + ec : 0.f;
-        }
-      float u[4][5];
-#pragma unroll
-      for (int b = 0; b < 5; ++b) {           // BT2 along rows
-        u[0][b] = d[0][b] - d[2][b];
-        u[1][b] = d[1][b] + d[2][b];
-        u[2][b] = d[2][b] - d[1][b];
-        u[3][b] = d[3][b] - d[1][b];
+      for (int p = 0; p < PER; ++p) {
+        const int i = lane + 64 * p;
+        if (i < NQ) *reinterpret_cast<f32x4*>(my + (i / Q4) * RS + (i % Q4) * 4) = rg[k][p];
       }
-      float* vb = V + ((size_t)(h * S4 + s4) * 4 + kq) * 64 + t * 4 + e;
-      constexpr int XSTRIDE = 2 * S4 * 4 * 64;  // floats between xi planes
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {           // BT3 along columns
-        const float* q = u[i];
-        vb[(i * 5 + 0) * XSTRIDE] = ((2.f * q[0] + q[1]) - 2.f * q[2]) - q[3];
-        vb[(i * 5 + 1) * XSTRIDE] = (2.f * q[1] + 3.f * q[2]) + q[3];
-        vb[(i * 5 + 2) * XSTRIDE] = (q[2] - 2.f * q[1]) + q[3];
-        vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
-        vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
+    } else {
+      for (int i = lane; i < 4 * (G::CELLS + 1); i += 64) {
+        const int ee = i / (G::CELLS + 1), j = i - ee * (G::CELLS + 1);
+        my[ee * RS + j] = j < G::CELLS ? src[(size_t)chan(quad, ee) * src_stride + j] : 0.f;  // + zero slot
       }
+    }
+    wave_lds_sync();
+    const float ec = emb ? eg[k] : 0.f;
+    const float* s = my + e * RS;
+    float d[4][5];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 5; ++b) {
+        // every lane reads (off-board taps read the zero slot, cell N*N):
+        // no exec-masked LDS reads, each waited for on its own
+        const int y = 2 * ty - 1 + a, x = 3 * tx - 1 + b;
+        const bool ok = tile && y >= 0 && y < G::N && x >= 0 && x < G::N;
+        const float v = s[ok ? y * G::N + x : G::CELLS];
+        d[a][b] = ok ? v + ec : 0.f;
+      }
+    float u[4][5];
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {             // BT2 along rows
+      u[0][b] = d[0][b] - d[2][b];
+      u[1][b] = d[1][b] + d[2][b];
+      u[2][b] = d[2][b] - d[1][b];
+      u[3][b] = d[3][b] - d[1][b];
+    }
+    float* vb = V + (size_t)quad * 64 + t * 4 + e;       // quad index == (h*S4 + s4)*4 + kq
+    constexpr int XSTRIDE = 2 * S4 * 4 * 64;  // floats between xi planes
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {             // BT3 along columns
+      const float* q = u[i];
+      vb[(i * 5 + 0) * XSTRIDE] = ((2.f * q[0] + q[1]) - 2.f * q[2]) - q[3];
+      vb[(i * 5 + 1) * XSTRIDE] = (2.f * q[1] + 3.f * q[2]) + q[3];
+      vb[(i * 5 + 2) * XSTRIDE] = (q[2] - 2.f * q[1]) + q[3];
+      vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
+      vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
     }
   }
   __syncthreads();
+  if (st) st->lap(21);
 }
 
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
@@ -212,7 +214,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   static_assert(2 * MT <= G::WAVES, "one wave per (cout tile, xi half)");
   constexpr int XG = kWinoXG;
   static_assert(XH % XG == 0, "xi groups");
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   const int m = wave >> 1, h = wave & 1;
   const bool active = wave < 2 * MT;

@@ -73,7 +73,7 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 24), np.uint64)
+    buf = np.zeros((G, 32), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
@@ -89,6 +89,7 @@ def stamps_report():
                       "wave_conv_loop": [round(float(v)) for v in waves if v > 0],
                       "stage_split": [round(float(v)) for v in allp[20:22]],
                       "select_split_root_deeper": [round(float(v)) for v in allp[22:24]],
+                      "root_level_split": [round(float(v)) for v in allp[24:28]],
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 
