@@ -96,6 +96,26 @@ def cpu_baseline(N, C, S, budget_s=12.0):
                       f"(oracle MCTS + torch-CPU batch-1 net; host has {os.cpu_count()} cpus)"}
 
 
+def _cpu_worker(a):
+    return cpu_baseline(*a)
+
+
+def cpu_baseline_procs(N, C, S, budget_s, procs):
+    """P independent single-thread oracle processes (the
+    reference's own parallelism is one game per process), sims/s summed.
+    Must run before this process touches the GPU (spawned children)."""
+    import multiprocessing as mp
+    if procs <= 1:
+        return cpu_baseline(N, C, S, budget_s)
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(N, C, S, budget_s)] * procs)
+    total = sum(r["value"] for r in res)
+    return {"value": total, "unit": "sims/s", "cores": procs, "kind": "port",
+            "single_core_value": res[0]["value"],
+            "sample": f"{procs} processes x 1 thread, each one {N}x{N} game at {S} sims/move for "
+                      f"{budget_s:.0f} s (oracle MCTS + torch-CPU batch-1 net; host has {os.cpu_count()} cpus)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,11 +127,17 @@ def main():
     ap.add_argument("--latent-dim", type=int, default=96)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+                    help="oracle processes for cpu_baseline (the GPU box's CPU share is 16)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu_ref = None
+    if world == 1 and not args.no_cpu_baseline:
+        # before the GPU is initialised: the baseline spawns worker processes
+        cpu_ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget, args.cpu_procs)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -122,7 +148,11 @@ def main():
     N, C, S, G = args.board_size, args.latent_dim, args.sims, args.games
     A = N * N + 1
     net = mzgo.MuZeroNet(C, A).to(f"cuda:{local}").eval()
-    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    if rank == 0:
+        net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    if world > 1:
+        from mzgo import distributed as mdist
+        mdist.broadcast_weights(net)                      # one RCCL broadcast, untimed
     sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G)
     eng = sp.engine
     M = sp.max_moves
@@ -217,8 +247,8 @@ def main():
                 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/summarize_profile.py)
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
                 out["roofline"]["traffic_source"] = f"profiles/{p['tag']}_summary.json"
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(N, C, S, args.cpu_budget)
+        if cpu_ref is not None:
+            out["cpu_baseline"] = cpu_ref
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -79,6 +79,24 @@ def gather_packed(buf, dst=0, group=None, to_host=True):
     return [p.cpu().numpy() for p in parts] if to_host else parts
 
 
+def broadcast_weights(module, src=0, group=None):
+    """Give every rank ``src``'s network: the whole state_dict flattened into
+    one f32 buffer and sent with a single broadcast (RCCL for CUDA modules;
+    0.75 MB at C=96).  Parameters are updated in place."""
+    sd = module.state_dict()
+    keys = sorted(sd)
+    dev = sd[keys[0]].device
+    flat = torch.cat([sd[k].detach().reshape(-1).to(device=dev, dtype=torch.float32) for k in keys])
+    dist.broadcast(flat, src=src, group=group)
+    off = 0
+    with torch.no_grad():
+        for k in keys:
+            n = sd[k].numel()
+            sd[k].copy_(flat[off:off + n].view(sd[k].shape).to(sd[k].dtype))
+            off += n
+    return module
+
+
 def gather_histories(engine, board_size, discount=0.99, dst=0, group=None):
     """Gather every rank's game records to ``dst`` as GameHistory objects,
     ordered by (rank, slot) == global game id under ``shard``."""

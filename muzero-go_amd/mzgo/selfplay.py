@@ -171,26 +171,58 @@ def main(argv=None):
     if (args.weights is None) == (args.random_init is None):
         ap.error("give exactly one of --weights or --random-init (self_play.py:531's default path is cluster-only)")
 
-    N = args.board_size
-    net = MuZeroNet(args.latent_dim, N * N + 1).to("cuda").eval()
-    if args.weights:
-        net.load_state_dict(torch.load(args.weights, map_location="cpu", weights_only=True))
-        print(f"Loaded weights from {args.weights}")
-    else:
-        net.load_state_dict(deterministic_state_dict(args.latent_dim, N * N + 1, args.random_init))
+    # one process per GPU under torchrun: games sharded by global id, weights
+    # broadcast from rank 0, finished games gathered to rank 0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
 
+        from . import distributed as mdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    N = args.board_size
+    net = MuZeroNet(args.latent_dim, N * N + 1).to(f"cuda:{local}").eval()
+    if rank == 0:
+        if args.weights:
+            net.load_state_dict(torch.load(args.weights, map_location="cpu", weights_only=True))
+            print(f"Loaded weights from {args.weights}")
+        else:
+            net.load_state_dict(deterministic_state_dict(args.latent_dim, N * N + 1, args.random_init))
+    if world > 1:
+        mdist.broadcast_weights(net)
+
+    # every rank plays the same number of games per round (gathers need equal
+    # buffers): ``per`` ids per rank, ids >= num_games are dropped on rank 0
+    per = -(-args.num_games // world)
+    base = rank * per
     histories = []
     t0 = time.time()
-    while len(histories) < args.num_games:
-        G = min(args.parallel_games, args.num_games - len(histories))
-        sp = SelfPlay(net, G, args.simulations, seed=args.seed, compat=args.compat,
-                      game_base=len(histories))
-        histories.extend(sp.play())
-        print(f"{len(histories)}/{args.num_games} games done")
+    done = 0
+    while done < per:
+        G = min(args.parallel_games, per - done)
+        sp = SelfPlay(net, G, args.simulations, seed=args.seed, compat=args.compat, game_base=base + done)
+        if world == 1:
+            histories.extend((base + done + g, h) for g, h in enumerate(sp.play()))
+        else:
+            sp.play()
+            got = mdist.gather_histories(sp.engine, N, sp.discount)
+            if rank == 0:
+                histories.extend((r * per + done + g, got[r * G + g]) for r in range(world) for g in range(G))
+        done += G
+        if rank == 0:
+            print(f"{min(done * world, args.num_games)}/{args.num_games} games done")
+    histories = [h for gid, h in sorted(histories, key=lambda x: x[0]) if gid < args.num_games]
     dt = time.time() - t0
-    save_batches(histories, args.output_dir, args.save_interval)
-    print(f"Finished {args.num_games} games in {dt:.2f} seconds.")
-    print(f"Average time per game: {dt / max(1, args.num_games):.2f} seconds.")
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        save_batches(histories, args.output_dir, args.save_interval)
+        print(f"Finished {args.num_games} games in {dt:.2f} seconds.")
+        print(f"Average time per game: {dt / max(1, args.num_games):.2f} seconds.")
 
 
 if __name__ == "__main__":

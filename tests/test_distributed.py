@@ -85,3 +85,34 @@ def test_gather_records_to_rank0_gloo():
         assert length == 2 + gid % 5
         assert actions == [gid] * length
         assert values == [gid / 10.0] * length
+
+
+def _bcast_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import mzgo
+        net = mzgo.MuZeroNet(96, N * N + 1)
+        net.load_state_dict(mzgo.deterministic_state_dict(96, N * N + 1, rank))   # ranks differ
+        mdist.broadcast_weights(net, src=0)
+        want = mzgo.deterministic_state_dict(96, N * N + 1, 0)
+        got = net.state_dict()
+        out.put((rank, max(float((got[k] - torch.as_tensor(want[k])).abs().max()) for k in want)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_weights_gloo():
+    """Every rank ends with rank 0's network after one flattened broadcast."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == {0: 0.0, 1: 0.0}
