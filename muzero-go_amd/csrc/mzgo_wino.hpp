@@ -220,7 +220,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   const bool active = wave < 2 * MT;
   const int kq = lane >> 4, t = lane & 15;
 
-  f32x4 yp[6];                                // Y partial [oy*3 + ox], component r = cout row
+  f32x4 yp[6];                                // Z [il*3 + ox] in the loop, then Y partial [oy*3 + ox]
 #pragma unroll
   for (int o = 0; o < 6; ++o) yp[o] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -276,36 +276,42 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
 #ifndef MZGO_DIAG_NOA
 #pragma unroll
         for (int q = 0; q < XG; ++q)
+#ifdef MZGO_DIAG_L1A
+          if (pos0 + q + PF < L) ar[(pos0 + q) % PF] = ap[((pos0 + q + PF) % 2) * 64];   // L1-resident (wrong values)
+#else
           if (pos0 + q + PF < L) ar[(pos0 + q) % PF] = ap[(pos0 + q + PF) * 64];
+#endif
 #endif
         // keep the refill loads here: left alone, the scheduler sinks them
         // next to their use (to save VGPRs) and exposes the L2 latency
         __builtin_amdgcn_sched_barrier(0);
       }
-      // fold M_xi into the output-tile partials: Y[oy][ox] += AT2[oy][i] AT3[ox][j] M
+      // fold M_xi along the columns: Z[il][ox] += AT3[ox][j] M_xi for
+      // xi = h*XH + xl, il = xl / 5, j = xl % 5 (the same for both halves);
+      // the rows (AT2) are applied once, after the loop
 #pragma unroll
       for (int q = 0; q < XG; ++q) {
-        const int xl = g * XG + q;
+        const int xl = g * XG + q, il = xl / 5, j = xl % 5;
         const f32x4 mv = acc[q];
 #pragma unroll
-        for (int oy = 0; oy < 2; ++oy)
-#pragma unroll
-          for (int ox = 0; ox < 3; ++ox) {
-            // xi = h*XH + xl: i = xi / 5, j = xi % 5 (h is wave-uniform; both
-            // halves are expanded at compile time and selected)
-            const float c0 = wino_at2(oy, xl / 5) * wino_at3(ox, xl % 5);
-            const float c1 = wino_at2(oy, (XH + xl) / 5) * wino_at3(ox, (XH + xl) % 5);
-            if (h == 0) {
-              if (c0 == 1.f) yp[oy * 3 + ox] += mv;
-              else if (c0 == -1.f) yp[oy * 3 + ox] -= mv;
-              else if (c0 != 0.f) yp[oy * 3 + ox] += c0 * mv;
-            } else {
-              if (c1 == 1.f) yp[oy * 3 + ox] += mv;
-              else if (c1 == -1.f) yp[oy * 3 + ox] -= mv;
-              else if (c1 != 0.f) yp[oy * 3 + ox] += c1 * mv;
-            }
-          }
+        for (int ox = 0; ox < 3; ++ox) {
+          const float cf = wino_at3(ox, j);
+          if (cf == 1.f) yp[il * 3 + ox] += mv;
+          else if (cf == -1.f) yp[il * 3 + ox] -= mv;
+          else if (cf != 0.f) yp[il * 3 + ox] += cf * mv;
+        }
       }
+    }
+  }
+  // rows: Y[oy][ox] = sum_i AT2[oy][i] Z[i][ox] over this half's i = 2h, 2h+1
+  // (AT2 = [[1,1,1,0],[0,1,-1,1]]): h = 0: Y0 = Z0 + Z1, Y1 = Z1;
+  // h = 1: Y0 = Z2, Y1 = Z3 - Z2.  yp[0..2] / yp[3..5] become Y[0] / Y[1].
+  if (active) {
+#pragma unroll
+    for (int ox = 0; ox < 3; ++ox) {
+      const f32x4 z0 = yp[ox], z1 = yp[3 + ox];
+      if (h == 0) { yp[ox] = z0 + z1; yp[3 + ox] = z1; }
+      else { yp[ox] = z0; yp[3 + ox] = z1 - z0; }
     }
   }
   if (st) { st->wave_add(8 + wave, __builtin_amdgcn_s_memtime() - t_loop); st->lap(6); }
