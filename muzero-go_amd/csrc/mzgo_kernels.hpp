@@ -97,7 +97,7 @@ struct Smem<G, true> {
     struct {
       float red[Wino<G>::template red_floats<G::C>()];
       float hp[(G::C / 16) * 3 * G::CS];
-      alignas(16) float outs[G::C * G::CS];           // conv output staging
+      alignas(16) float outs[G::C * Wino<G>::OUT_STRIDE];   // conv output staging
     } x;
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
   } u;

@@ -53,6 +53,9 @@ struct Wino {
   static constexpr int T = TY * TX;           // tiles (MFMA columns)
   static constexpr int XI = 20;               // 4 x 5 transform points
   static_assert(T <= 16, "tiles must fit one MFMA column tile");
+  // output staging row stride: 4 cout rows apart (the kq lane groups) land 16
+  // banks apart instead of on the same bank
+  static constexpr int OUT_STRIDE = G::CS + (36 - G::CS % 32) % 32;
   // V floats for CIN input channels: [xi][h][s4][kq][t16][e4]
   template <int CIN>
   static constexpr int v_floats() { return XI * CIN * 16; }
@@ -207,6 +210,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
                                           Stamp* st = nullptr) {
   typedef Wino<G> W;
   constexpr int CH = CIN / 2, S4 = CH / 16, MT = COUT / 16, XI = W::XI;
+  constexpr int OS = W::OUT_STRIDE;
   constexpr int XH = XI / 2;                  // xi per wave (two xi halves)
   constexpr int KP = CIN / 16;                // float4 k-positions per xi (4 k-steps each)
   constexpr int L = XH * KP;                  // float4 A loads (and B reads) per wave
@@ -362,7 +366,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         v = v > 0.f ? v : 0.f;
         v = valid ? v : 0.f;
         const int co = m * 16 + kq * 4 + r;
-        if (valid) outs[co * G::CS + cell] = v;      // staged for a coalesced store
+        if (valid) outs[co * OS + cell] = v;         // staged for a coalesced store
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) hsum[hh][ox] = __builtin_fmaf(hw[hh][r], v, hsum[hh][ox]);
       }
@@ -383,7 +387,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   // pad cells of the staged rows are 0 (the pooled layout keeps them 0)
   for (int i = threadIdx.x; i < COUT * (G::CS - G::CELLS); i += G::THREADS) {
     const int co = i / (G::CS - G::CELLS);
-    outs[co * G::CS + G::CELLS + (i - co * (G::CS - G::CELLS))] = 0.f;
+    outs[co * OS + G::CELLS + (i - co * (G::CS - G::CELLS))] = 0.f;
   }
   __syncthreads();
   // whole-row stores (the tile-ordered epilogue would scatter 4-byte writes)
@@ -391,7 +395,8 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     if (out_stride == G::CS && out_cells == G::CS) {
       constexpr int Q = G::CS / 4;
       for (int i = threadIdx.x; i < COUT * Q; i += G::THREADS) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(outs + i * 4);
+        const int co = i / Q, q = i - co * Q;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(outs + co * OS + q * 4);
 #if MZGO_NT_STORE
         __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out) + i);
 #else
@@ -401,7 +406,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     } else {
       for (int i = threadIdx.x; i < COUT * out_cells; i += G::THREADS) {
         const int co = i / out_cells, j = i - co * out_cells;
-        out[(size_t)co * out_stride + j] = outs[co * G::CS + j];
+        out[(size_t)co * out_stride + j] = outs[co * OS + j];
       }
     }
   }
