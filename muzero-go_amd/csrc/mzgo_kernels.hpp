@@ -192,6 +192,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                                  float* latent, float* value, float* logits) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int b = blockIdx.x;
   const float* o = obs + (size_t)b * 6 * G::CELLS;
   float* lat = latent + (size_t)b * G::C * G::CELLS;
@@ -207,6 +208,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                                    float* value, float* logits, int* err) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int b = blockIdx.x;
   int64_t a = action[b];
   if (a < 0 || a >= G::A) {            // nn.Embedding would raise IndexError
@@ -320,6 +322,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                       int move_index, int* out_visits, double* out_value) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int g = blockIdx.x;
   const float* o = root_obs + (size_t)g * 6 * G::CELLS;
   const uint64_t key = stream_key(sp.seed, (uint32_t)(game_base + g), (uint32_t)move_index);
@@ -536,6 +539,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                              EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int g = blockIdx.x;
   if (E.status[g] != 0) return;
   BoardMeta m;

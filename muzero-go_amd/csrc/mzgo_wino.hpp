@@ -56,6 +56,7 @@ struct Wino {
   // output staging row stride: 4 cout rows apart (the kq lane groups) land 16
   // banks apart instead of on the same bank
   static constexpr int OUT_STRIDE = G::CS + (36 - G::CS % 32) % 32;
+  static_assert(OUT_STRIDE > G::CS, "junk cell CS past the stored row");
   // V floats for CIN input channels: [xi][h][s4][kq][t16][e4]
   template <int CIN>
   static constexpr int v_floats() { return XI * CIN * 16; }
@@ -73,22 +74,38 @@ struct Wino {
 // Work unit: a channel quad (h, s4, kq) = the 4 channels e = 0..3 that share
 // one V row; lane (t, e) transforms tile t of channel e.  Each wave fetches
 // its quads' rows itself (coalesced 16-byte loads, all in flight at once) and
-// stages them in its own slice of raw ([4][RAW_STRIDE] per wave), so the only
-// workgroup barrier is the one before the GEMM.  Cell N*N of each raw row is
-// 0 (pooled latents keep 0 in their pad cells).  All threads; returns
-// synchronised.
+// scatters them, embedding already added, into its own slice of raw: one
+// zero-haloed (N+3) x (N+2) plane per channel (rows -1..N+1, cols -1..N), so
+// every tap of every tile is a plain load at a constant offset -- no bounds
+// selects.  The only workgroup barrier is the one before the GEMM.
 template <class G>
 struct WinoRaw {
-  static constexpr int STRIDE = G::CS + (36 - G::CS % 32) % 32;  // >= CS, == 4 mod 32
-  static constexpr int FLOATS = G::WAVES * 4 * STRIDE;             // all waves' slices
+  static_assert(G::N == 9, "bank layout derived for 9x9 tiles");
+  static constexpr int PW = G::N + 2;                    // padded width
+  static constexpr int PH = 2 * Wino<G>::TY + 2;         // padded height (last tile row + halo)
+  static constexpr int PLANE = PH * PW;
+  // plane stride == 11 (mod 32): lanes of channels e and e+1 (one 32-lane
+  // half) then share only 2 of their 15 tile banks (offsets 22*ty + 3*tx)
+  static constexpr int STRIDE = PLANE + ((11 - PLANE % 32) % 32 + 32) % 32;
+  static_assert(STRIDE > PLANE, "a junk slot past each plane");
+  static constexpr int FLOATS = G::WAVES * 4 * STRIDE;   // all waves' slices
 };
+
+// The halo of every raw plane must be 0 before the first wino_input of a
+// kernel (it is never written afterwards).  All threads; synchronises.
+template <class G>
+__device__ __forceinline__ void wino_raw_zero(float* raw) {
+  for (int i = threadIdx.x; i < WinoRaw<G>::FLOATS; i += G::THREADS) raw[i] = 0.f;
+  __syncthreads();
+}
 
 template <class G, int CIN>
 __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restrict__ raw,
                                            const float* __restrict__ src, int src_stride,
                                            const float* __restrict__ emb, Stamp* st = nullptr) {
   typedef Wino<G> W;
-  constexpr int CH = CIN / 2, S4 = CH / 16, RS = WinoRaw<G>::STRIDE;
+  typedef WinoRaw<G> R;
+  constexpr int CH = CIN / 2, S4 = CH / 16, RS = R::STRIDE, PW = R::PW;
   static_assert(CIN % 32 == 0, "two cin halves of whole 4-k-step groups");
   constexpr int QUADS = 2 * S4 * 4;           // (h, s4, kq)
   constexpr int QPW = (QUADS + G::WAVES - 1) / G::WAVES;   // quads per wave
@@ -98,34 +115,43 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
   const int lane = lane_id_local();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   const int t = lane & 15, e = lane >> 4;
-  const int ty = t / W::TX, tx = t - ty * W::TX;
-  const bool tile = t < W::T;
+  const int tt = t < W::T ? t : W::T - 1;     // pad column: any valid tile (output unused)
+  const int ty = tt / W::TX, tx = tt - ty * W::TX;
   const bool pooled = src_stride == G::CS;
   float* my = raw + wave * 4 * RS;
   auto chan = [&](int quad, int ee) {         // channel of quad member ee
     const int h = quad / (S4 * 4), s4 = (quad / 4) % S4, kq = quad % 4;
     return h * CH + 4 * (4 * s4 + ee) + kq;
   };
+  auto pidx = [&](int cell) { const int y = cell / G::N; return (y + 1) * PW + (cell - y * G::N) + 1; };
 
-  // all of this wave's rows in flight at once; loads are branch-free
-  // (clamped indices) so the compiler keeps them outstanding together
+  // all of this wave's rows (and their embedding values) in flight at once;
+  // loads are branch-free (clamped indices) so they stay outstanding together
   f32x4 rg[QPW][PER];
-  float eg[QPW];
+  float eg[QPW][PER];
   const f32x4* s4p = reinterpret_cast<const f32x4*>(src);
   const float* ebase = emb ? emb : src;
 #pragma unroll
   for (int k = 0; k < QPW; ++k) {
     const int quad = min(wave + k * G::WAVES, QUADS - 1);
-    if (pooled) {
 #pragma unroll
-      for (int p = 0; p < PER; ++p) {
-        const int i = min(lane + 64 * p, NQ - 1);
-        rg[k][p] = s4p[chan(quad, i / Q4) * Q4 + i % Q4];
-      }
+    for (int p = 0; p < PER; ++p) {
+      const int i = min(lane + 64 * p, NQ - 1);
+      if (pooled) rg[k][p] = s4p[chan(quad, i / Q4) * Q4 + i % Q4];
+      eg[k][p] = ebase[chan(quad, i / Q4)];
     }
-    eg[k] = ebase[chan(quad, e)];
   }
   if (st) st->lap(20);
+  // scatter targets of this lane's 4*PER floats (pad cells and surplus lanes
+  // go to a junk slot past the plane): the same for every quad
+  int widx[PER][4];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int i = lane + 64 * p, ee = min(i, NQ - 1) / Q4, c0 = (min(i, NQ - 1) % Q4) * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      widx[p][r] = (i < NQ && c0 + r < G::CELLS) ? ee * RS + pidx(c0 + r) : R::PLANE;
+  }
 
 #pragma unroll
   for (int k = 0; k < QPW; ++k) {
@@ -135,30 +161,24 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
     if (pooled) {
 #pragma unroll
       for (int p = 0; p < PER; ++p) {
-        const int i = lane + 64 * p;
-        if (i < NQ) *reinterpret_cast<f32x4*>(my + (i / Q4) * RS + (i % Q4) * 4) = rg[k][p];
+        const float ec = emb ? eg[k][p] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) my[widx[p][r]] = rg[k][p][r] + ec;
       }
     } else {
-      for (int i = lane; i < 4 * (G::CELLS + 1); i += 64) {
-        const int ee = i / (G::CELLS + 1), j = i - ee * (G::CELLS + 1);
-        my[ee * RS + j] = j < G::CELLS ? src[(size_t)chan(quad, ee) * src_stride + j] : 0.f;  // + zero slot
+      for (int i = lane; i < 4 * G::CELLS; i += 64) {
+        const int ee = i / G::CELLS, j = i - ee * G::CELLS;
+        const float ec = emb ? emb[chan(quad, ee)] : 0.f;
+        my[ee * RS + pidx(j)] = src[(size_t)chan(quad, ee) * src_stride + j] + ec;
       }
     }
     wave_lds_sync();
-    const float ec = emb ? eg[k] : 0.f;
-    const float* s = my + e * RS;
+    const float* s = my + e * RS + (2 * ty) * PW + 3 * tx;   // tile's top-left (padded coords)
     float d[4][5];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 5; ++b) {
-        // every lane reads (off-board taps read the zero slot, cell N*N):
-        // no exec-masked LDS reads, each waited for on its own
-        const int y = 2 * ty - 1 + a, x = 3 * tx - 1 + b;
-        const bool ok = tile && y >= 0 && y < G::N && x >= 0 && x < G::N;
-        const float v = s[ok ? y * G::N + x : G::CELLS];
-        d[a][b] = ok ? v + ec : 0.f;
-      }
+      for (int b = 0; b < 5; ++b) d[a][b] = s[a * PW + b];
     float u[4][5];
 #pragma unroll
     for (int b = 0; b < 5; ++b) {             // BT2 along rows
@@ -334,12 +354,19 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   __syncthreads();                            // V is dead: red may overwrite it
   // wave (m, h) hands its partial of output row oy = 1 - h to its partner
   // (the other xi half of the same cout tile)
+  // (rows picked by a wave-uniform select, not a dynamic register index)
+  f32x4 ymine[3], ygive[3];
+#pragma unroll
+  for (int ox = 0; ox < 3; ++ox) {
+    ymine[ox] = h == 0 ? yp[ox] : yp[3 + ox];
+    ygive[ox] = h == 0 ? yp[3 + ox] : yp[ox];
+  }
   if (active) {
 #pragma unroll
     for (int ox = 0; ox < 3; ++ox)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        red[((m * 2 + h) * 12 + ox * 4 + r) * 64 + lane] = yp[(1 - h) * 3 + ox][r];
+        red[((m * 2 + h) * 12 + ox * 4 + r) * 64 + lane] = ygive[ox][r];
   }
   __syncthreads();
   if (st) st->lap(7);
@@ -360,13 +387,13 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float other = red[((m * 2 + (1 - h)) * 12 + ox * 4 + r) * 64 + lane];
-        const float mine = yp[oy * 3 + ox][r];
+        const float mine = ymine[ox][r];
         // fixed order: (xi half 0) + (xi half 1)
         float v = (h == 0 ? mine + other : other + mine) + bb[r];
         v = v > 0.f ? v : 0.f;
         v = valid ? v : 0.f;
         const int co = m * 16 + kq * 4 + r;
-        if (valid) outs[co * OS + cell] = v;         // staged for a coalesced store
+        outs[co * OS + (valid ? cell : G::CS)] = v;  // staged (off-board lanes: junk cell CS)
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) hsum[hh][ox] = __builtin_fmaf(hw[hh][r], v, hsum[hh][ox]);
       }

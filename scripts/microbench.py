@@ -90,6 +90,7 @@ def stamps_report():
                       "stage_split": [round(float(v)) for v in allp[20:22]],
                       "select_split_root_deeper": [round(float(v)) for v in allp[22:24]],
                       "root_level_split": [round(float(v)) for v in allp[24:28]],
+                      "stage_load_wait": round(float(allp[28])),
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 
