@@ -88,3 +88,32 @@ def test_sampled_dirichlet_statistics():
     want_var = (1 / A) * (1 - 1 / A) / (A * alpha + 1)
     assert abs(mean - 1 / A) < 1e-9
     assert 0.7 * want_var < var < 1.3 * want_var, (var, want_var)
+
+
+@pytest.mark.parametrize("N,S,moves", [(6, 64, 0), (6, 64, 9), (9, 100, 14), (9, 100, 30)])
+def test_search_matches_oracle_tree(N, S, moves):
+    """Sizes / positions without a reference golden (6x6 is self_play.py's
+    default board, :20): the device tree vs the oracle's restatement of
+    MCTS.run (itself pinned to the reference goldens above), same hooks."""
+    import mzgo
+    from oracle.mcts import MCTS, tree_summary
+    from oracle.net import OracleNet
+    from oracle.positions import random_position
+    from oracle.rng import SearchHooks, injected_noise
+    from oracle.weights import deterministic_state_dict
+    C, A, seed, game, move = 96, N * N + 1, 31, 2, moves
+    obs = random_position(N, moves, 100 + moves) if moves else np.zeros((6, N, N))
+    noise = injected_noise(seed, game, move, A)
+    hooks = SearchHooks(seed, game, move)
+    onet = OracleNet(deterministic_state_dict(C, A, 0))
+    ref = MCTS(onet, A, S, choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+               noise=lambda p, a, e: (1 - e) * p + e * noise)
+    with torch.no_grad():
+        r_root, _, r_value = ref.run(obs)
+    r_visits, r_depth = tree_summary(r_root, A)
+    mcts = mzgo.MCTS(_net(N), A, S, seed=seed, game=game)
+    root, _, value = mcts.run(obs, move_index=move, noise=torch.from_numpy(noise))
+    visits, depth = tree_summary(root, A)
+    np.testing.assert_array_equal(visits, r_visits)
+    np.testing.assert_array_equal(np.array(depth), np.array(r_depth))
+    assert abs(value - r_value) < 1e-5
