@@ -20,6 +20,7 @@ Fixtures:
   game_5x5_*.npz/json  a reference run_self_play_game (self_play.py:453) over
                        oracle.goenv.GoEnv, (a) with counter-stream hooks and
                        (b) with the reference's own seeded RNGs
+  mctsmain_*.npz       main.py's MCTS.run (main.py:246-368) under the same hooks
 Usage:  python -m oracle.make_golden   (from the repo root)
 """
 import json
@@ -187,6 +188,53 @@ def make_mcts(sp, name, N, S, n_moves, seed=11, game=3, move=5, C=96):
     print("mcts", name, "root N", root.visit_count, "value", rv, "depth", depth)
 
 
+def make_mcts_main(mn, name, N, S, n_moves, seed=13, game=4, move=6, C=96):
+    """main.py's MCTS (main.py:246-368; trainer self-play and arena), same
+    counter-stream hooks: random.choice -> TAG_SELECT per simulation (the
+    simulation index counted by wrapping select_leaf, called once per
+    simulation at :290), apply_dirichlet_noise -> injected sample."""
+    from oracle.mcts import tree_summary
+    from oracle.positions import random_position
+    from oracle.rng import SearchHooks, injected_noise
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    mn.config.board_size = N
+    mn.config.max_action_size = A
+    sd = deterministic_state_dict(C, A, 0)
+    net = mn.MuZeroNet(C, A)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net.eval()
+    obs = random_position(N, n_moves, seed=700 + n_moves)
+    hooks = SearchHooks(seed, game, move)
+    state = {"sim": -1}
+    saved = (mn.random.choice, mn.apply_dirichlet_noise, mn.MCTS.select_leaf)
+    orig_select = mn.MCTS.select_leaf
+
+    def select_leaf(self_, node):
+        state["sim"] += 1
+        return orig_select(self_, node)
+
+    def noise(policy, alpha, epsilon):
+        return (1 - epsilon) * policy + epsilon * injected_noise(seed, game, move, len(policy))
+    mn.random.choice = lambda seq: seq[hooks.choice_index(len(seq), state["sim"])]
+    mn.apply_dirichlet_noise = noise
+    mn.MCTS.select_leaf = select_leaf
+    try:
+        with torch.no_grad():
+            root = mn.MCTS(net, A, S).run(obs)
+    finally:
+        mn.random.choice, mn.apply_dirichlet_noise, mn.MCTS.select_leaf = saved
+    visits, depth = tree_summary(root, A)
+    priors = np.array([float(root.children[a]["prior"]) for a in range(A)], dtype=np.float64)
+    out = dict(obs=obs, visits=visits, root_value=np.float64(root.value()), root_n=np.int64(root.visit_count),
+               root_priors=priors, depth_hist=np.array(depth, dtype=np.int64), seed=np.int64(seed),
+               game=np.int64(game), move=np.int64(move), S=np.int64(S), N=np.int64(N), C=np.int64(C),
+               c_puct=np.float64(2.0), pass_epsilon=np.float64(mn.config.pass_epsilon),
+               dirichlet_epsilon=np.float64(mn.config.dirichlet_epsilon), discount=np.float64(mn.config.discount))
+    np.savez_compressed(os.path.join(GOLDEN, f"mctsmain_{name}.npz"), **out)
+    print("mcts(main.py)", name, "root N", root.visit_count, "value", root.value(), "depth", depth)
+
+
 def _pack_record(rec):
     types = {
         "rewards": [type(r).__name__ for r in rec["rewards"]],
@@ -264,7 +312,23 @@ def main():
     make_mcts(sp, "19x19_s800_mid", 19, 800, 120)
     make_game(sp, "5x5_s25_hooked", hooked=True)
     make_game(sp, "5x5_s25_seeded", hooked=False)
+    import main as mn  # noqa: E402  (the reference trainer module, same stubs)
+    make_mcts_main(mn, "5x5_s25_mid", 5, 25, 7)
+    make_mcts_main(mn, "9x9_s200_empty", 9, 200, 0)
+    make_mcts_main(mn, "9x9_s200_mid", 9, 200, 26)
+
+
+def main_only():
+    """Regenerate only the main.py MCTS fixtures (``python -m oracle.make_golden main``)."""
+    os.makedirs(GOLDEN, exist_ok=True)
+    sys.path.insert(0, REPO)
+    import_reference()
+    torch.set_num_threads(1)
+    import main as mn  # noqa: E402
+    make_mcts_main(mn, "5x5_s25_mid", 5, 25, 7)
+    make_mcts_main(mn, "9x9_s200_empty", 9, 200, 0)
+    make_mcts_main(mn, "9x9_s200_mid", 9, 200, 26)
 
 
 if __name__ == "__main__":
-    main()
+    main_only() if sys.argv[1:] == ["main"] else main()

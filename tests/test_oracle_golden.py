@@ -126,3 +126,29 @@ def test_selfplay_game_matches_reference(golden_dir, mode):
         agent = Agent(net, N, A, S)
     hist = run_self_play_game(agent, GoEnv(N), N, hooks_factory=factory)
     _check_record(hist, g, types)
+
+
+@pytest.mark.parametrize("case", ["5x5_s25_mid", "9x9_s200_empty", "9x9_s200_mid"])
+def test_main_variant_mcts_matches_reference_tree(golden_dir, case):
+    """oracle.mcts_main (main.py:246-368 restated) vs trees recorded from the
+    reference main.py MCTS under the same counter-stream hooks."""
+    from oracle.mcts_main import MCTSMain
+    g = np.load(os.path.join(golden_dir, f"mctsmain_{case}.npz"))
+    N, S, C = int(g["N"]), int(g["S"]), int(g["C"])
+    seed, game, move = int(g["seed"]), int(g["game"]), int(g["move"])
+    A = N * N + 1
+    hooks = SearchHooks(seed, game, move)
+    noise = injected_noise(seed, game, move, A)
+    m = MCTSMain(OracleNet(deterministic_state_dict(C, A, 0)), A, S, c_puct=float(g["c_puct"]),
+                 dirichlet_epsilon=float(g["dirichlet_epsilon"]), pass_epsilon=float(g["pass_epsilon"]),
+                 discount=float(g["discount"]),
+                 choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+                 noise=lambda p, a, e: (1 - e) * p + e * noise)
+    with torch.no_grad():
+        root = m.run(g["obs"])
+    visits, depth = tree_summary(root, A)
+    np.testing.assert_array_equal(visits, g["visits"])
+    np.testing.assert_array_equal(np.array(depth), g["depth_hist"])
+    np.testing.assert_array_equal([float(root.children[a]["prior"]) for a in range(A)], g["root_priors"])
+    assert root.visit_count == int(g["root_n"])
+    assert abs(root.value() - float(g["root_value"])) < 1e-12
