@@ -52,8 +52,9 @@ typedef struct mzgo_config {
   int max_moves;            /* move cap, N*N in the reference (self_play.py:461); 0 = N*N */
   int compat;               /* 0 = reference (zero visit counts, §0.6), 1 = fixed */
   int temperature_moves;    /* 15 (self_play.py:29) */
-  int reserved;
-  double c_puct;            /* 2.5 (self_play.py:143) */
+  int search_variant;       /* 0 = self_play.py's MCTS (:142-343), 1 = main.py's MCTS
+                               (main.py:246-368: trainer self-play and arena rules) */
+  double c_puct;            /* 2.5 (self_play.py:143); main.py's variant uses 2 */
   double discount;          /* 0.99 */
   double dirichlet_alpha;   /* 0.15 */
   double dirichlet_epsilon; /* 0.02 */

@@ -238,6 +238,7 @@ struct mzgo_engine {
     sp.c_puct = cfg.c_puct; sp.discount = cfg.discount;
     sp.dirichlet_alpha = cfg.dirichlet_alpha; sp.dirichlet_epsilon = cfg.dirichlet_epsilon;
     sp.pass_epsilon = cfg.pass_epsilon; sp.num_simulations = S; sp.compat = cfg.compat;
+    sp.variant = cfg.search_variant;
     sp.seed = cfg.seed;
     return sp;
   }
@@ -275,6 +276,8 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   if (cfg->num_games < 1) return fail(MZGO_EINVAL, "num_games must be >= 1");
   if (C != 0 && cfg->num_simulations < 1) return fail(MZGO_EINVAL, "num_simulations must be >= 1");
   if (cfg->compat != 0 && cfg->compat != 1) return fail(MZGO_EINVAL, "compat must be 0 or 1");
+  if (cfg->search_variant != 0 && cfg->search_variant != 1)
+    return fail(MZGO_EINVAL, "search_variant must be 0 (self_play.py) or 1 (main.py)");
   HIPCHK(hipSetDevice(cfg->device));
   auto* e = new mzgo_engine();
   e->cfg = *cfg;

@@ -247,7 +247,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     st.lap(0);
     const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;
     if (a < 0) {                                         // terminal leaf: backup 0 (:188-191)
-      if (wave_id() == 0) backup<G>(T, depth, -1, 0.0);
+      // self_play.py: terminal leaf -> backup 0 (:188-191); main.py: nothing (:296)
+      if (wave_id() == 0 && a == -1) backup<G>(T, depth, -1, 0.0);
       __syncthreads();
       continue;
     }
@@ -263,7 +264,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     // its tree loads never wait for store acks.  The select barrier joins them.
     if (wave_id() == 1) {
       heads_logits<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, sm.t.logits);
-      child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A, nid);
+      child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A, nid, sp.variant);
       int* crow = TV.child + (size_t)nid * G::A;      // the new node: no children yet
       for (int i = lane_id(); i < G::A; i += 64) crow[i] = -1;
     }
@@ -271,7 +272,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       float r, v;
       heads_value<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, r, v);
       if (lane_id() == (a & 63)) T.set_child(leaf, a, nid);
-      backup<G>(T, depth, nid, (double)r + sp.discount * (double)v);
+      backup<G>(T, depth, nid, (double)r + sp.discount * (double)v, sp.variant == 0);
     }
     st.lap(3);
   }
@@ -424,6 +425,58 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 // Action choice (MuZeroAgent.select_action, self_play.py:357-402).  Wave 0.
 // Writes the policy target to pol[A]; returns the action.
 // ---------------------------------------------------------------------------
+// main.py's move rule (self-play :660-673 and the arena evaluator :552-565):
+// visit_counts = child visit counts where valid_mask > 0; argmax (first max)
+// with policy = counts / sum, else random.choice(valid actions) with a one-hot
+// policy.  Temperature plays no part.  Wave 0.
+template <class G>
+__device__ __forceinline__ int choose_action_main(TreeLds<G>& t, const TreeView& T, uint64_t key, double* pol) {
+  const int lane = lane_id_local();
+  double vc[G::AP];
+  double bv = -1.0, tot = 0.0;
+  int ba = 0x7fffffff, best_c = 0;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    vc[j] = 0.0;
+    if (a < G::A && mask_of<G>(t, a) > 0) { const int c = T.child[a]; vc[j] = c >= 0 ? (double)T.visits[c] : 0.0; }
+    tot += vc[j];
+    if (a < G::A && (vc[j] > bv || (vc[j] == bv && a < ba))) { bv = vc[j]; ba = a; }
+  }
+  tot = wave_sum(tot);                          // integer counts: exact in any order
+  wave_argmax(bv, ba, best_c);
+  int action = ba;
+  if (!(tot > 0)) {                             // random.choice(valid actions)
+    uint64_t vb[G::AP];
+    int nvalid = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      vb[j] = __ballot(a < G::A && mask_of<G>(t, a) > 0);
+      nvalid += __popcll(vb[j]);
+    }
+    uint32_t k = randbelow(draw(key, TAG_ACTION, 0), (uint32_t)nvalid);
+    action = -1;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const uint32_t c = __popcll(vb[j]);
+      if (action < 0 && k < c) {
+        uint64_t mm = vb[j];
+        for (uint32_t i = 0; i < k; ++i) mm &= mm - 1;
+        action = 64 * j + __ffsll((long long)mm) - 1;
+      } else if (action < 0) {
+        k -= c;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    if (a < G::A) pol[a] = tot > 0 ? vc[j] / tot : (a == action ? 1.0 : 0.0);
+  }
+  return action;
+}
+
 template <class G>
 __device__ __forceinline__ int choose_action(TreeLds<G>& t, const TreeView& T, int compat, double temperature,
                                     uint64_t key, double* pol) {
@@ -561,7 +614,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const TreeView T = TreeViewOf<G>::make(E, g);
   if (wave_id() == 0) {
     const double temp = mv < pp.temperature_moves ? pp.temperature : 0.0;
-    const int a = choose_action<G>(sm.t, T, sp.compat, temp, key, E.rec_policy + rec * G::A);
+    const int a = sp.variant == 1 ? choose_action_main<G>(sm.t, T, key, E.rec_policy + rec * G::A)
+                                  : choose_action<G>(sm.t, T, sp.compat, temp, key, E.rec_policy + rec * G::A);
     if (lane_id() == 0) {
       sm.bc[0] = a;
       E.rec_action[rec] = a;

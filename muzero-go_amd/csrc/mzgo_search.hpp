@@ -24,6 +24,7 @@ struct SearchParams {
   double pass_epsilon;      // 0.01
   int num_simulations;      // S
   int compat;               // 0: reference (zero visit counts), 1: fixed
+  int variant;              // 0: self_play.py MCTS, 1: main.py MCTS (main.py:246-368)
   uint64_t seed;
 };
 
@@ -233,9 +234,21 @@ __device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward,
 // Child priors of a new node (self_play.py:204-224): p = softmax * root mask,
 // normalised by numpy's f32 pairwise sum; entries with mask 0 are 0.  Wave 0.
 template <class G>
-__device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst, int node = -1) {
+__device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst, int node = -1,
+                                             int variant = 0) {
   const int lane = lane_id_local();
   softmax_wave<G>(t);
+  if (variant == 1) {
+    // main.py:299-309: softmax[a] where valid_mask[a] > 0, not renormalised
+    for (int a = lane; a < G::A; a += 64) {
+      const float p = mask_of<G>(t, a) > 0 ? t.fbuf[a] : 0.f;
+      dst[a] = p;
+      if (node >= 0) t.newp[a] = p;
+    }
+    if (node >= 0 && lane == 0)
+      __hip_atomic_store(&t.newp_node, node, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
   const float s = np_pairwise_sum<float, G::A>(t.fbuf);
   if (s > 0.f) {
@@ -299,6 +312,22 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
   }
   const double eps = sp.dirichlet_epsilon;
   const float keep32 = (float)(1.0 - eps);   // Python float * f32 array -> f32 (NEP 50)
+  if (sp.variant == 1) {
+    // main.py:266-287: normalise only if the sum is positive, mix the noise,
+    // keep p[a] where valid_mask[a] > 0 -- no re-mask, no renormalisation
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      if (a < G::A) {
+        const float p = s > 0.f ? t.fbuf[a] / s : t.fbuf[a];
+        const double q = (double)(keep32 * p) + eps * t.dbuf[a];
+        const double pr = mask_of<G>(t, a) > 0 ? q : 0.0;
+        T.root_prior[a] = pr;
+        if (G::TREE_CAP > 0) t.rprior[a] = pr;
+      }
+    }
+    return;
+  }
   double q[G::AP];
   if (s > 0.f) {
 #pragma unroll
@@ -401,7 +430,13 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) any_elig |= elig[j];
     if (st && root) st->lap(24);
-    if ((nvis > 0 && !anypos) || !any_elig) { t.leaf = node; t.depth = depth; return -1; }
+    if (sp.variant == 1) {
+      // main.py:318-364 has no terminal test; with no positive-prior child the
+      // walk ends without an action and the simulation does nothing (:296)
+      if (!any_elig) { t.leaf = node; t.depth = depth; return -2; }
+    } else if ((nvis > 0 && !anypos) || !any_elig) {
+      t.leaf = node; t.depth = depth; return -1;
+    }
 
     if (n_unexp > 0) {
       // random.choice over the ascending list of unexpanded eligible actions
@@ -443,7 +478,8 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     lo = wave_min(lo);
     hi = wave_max(hi);
     if (st && root) st->lap(26);
-    const double sq = sqrt((double)(nvis > 1 ? nvis : 1));
+    // sqrt(max(1, N)) (self_play.py:316) or sqrt(N + 1) (main.py:354)
+    const double sq = sp.variant == 1 ? sqrt((double)(nvis + 1)) : sqrt((double)(nvis > 1 ? nvis : 1));
     double best_s = -INFINITY;
     int best_a = 0x7fffffff, best_c = -1;
 #pragma unroll
@@ -460,7 +496,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     }
     if (st && root) st->lap(27);
     wave_argmax(best_s, best_a, best_c);
-    if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return -1; }
+    if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return sp.variant == 1 ? -2 : -1; }
     depth += 1;
     if (lane == 0) const_cast<Acc&>(T).set_path(depth, best_c);
     node = best_c;
@@ -475,13 +511,14 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
 // +v, alternating sign upward (self_play.py:337-343).  Wave 0; path nodes are
 // distinct, so each lane updates its own node.  Path entry 0 is the root.
 template <class G, class Acc>
-__device__ __forceinline__ void backup(Acc& T, int depth, int nid, double v) {
+__device__ __forceinline__ void backup(Acc& T, int depth, int nid, double v, bool alternate = true) {
   const int lane = lane_id_local();
   const int off = nid >= 0 ? 1 : 0;
   const int count = depth + 1 + off;              // nodes on the backed-up path
   for (int i = lane; i < count; i += 64) {
     const int node = (off && i == 0) ? nid : T.path(depth - (i - off));
-    T.add(node, (i & 1) ? -v : v);
+    // self_play.py:337-343 alternates the sign; main.py:366-368 does not
+    T.add(node, (alternate && (i & 1)) ? -v : v);
   }
   wave_lds_sync();
 }

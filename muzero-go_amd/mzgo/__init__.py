@@ -5,6 +5,7 @@ self_play.py), all executed by libmzgo.so's HIP kernels:
 
 * ``MuZeroNet``   -- same parameters/state_dict keys; initial/recurrent inference on MFMA
 * ``MCTS``, ``MuZeroAgent`` -- device search (select / expand / backup kernels)
+* ``MainMCTS`` -- main.py's MCTS variant (trainer self-play / arena) on the same kernels
 * ``GoEnv``       -- GymGo rules as bit-exact integer kernels
 * ``SelfPlay``    -- G concurrent games per GPU, one fused kernel step per move
 * ``GameHistory``, ``save_batches`` -- the reference's record / pickle format
@@ -12,9 +13,9 @@ self_play.py), all executed by libmzgo.so's HIP kernels:
 from .engine import Engine, EngineConfig
 from .env import GoEnv
 from .net import MuZeroNet
-from .search import MCTS, MuZeroAgent
+from .search import MCTS, MainMCTS, MuZeroAgent
 from .selfplay import GameHistory, SelfPlay, history_from_device, save_batches
 from .weights import deterministic_state_dict
 
-__all__ = ["Engine", "EngineConfig", "GoEnv", "MuZeroNet", "MCTS", "MuZeroAgent", "SelfPlay",
+__all__ = ["Engine", "EngineConfig", "GoEnv", "MuZeroNet", "MCTS", "MainMCTS", "MuZeroAgent", "SelfPlay",
            "GameHistory", "history_from_device", "save_batches", "deterministic_state_dict"]

@@ -28,7 +28,7 @@ class Config(ctypes.Structure):
         ("max_moves", ctypes.c_int),
         ("compat", ctypes.c_int),
         ("temperature_moves", ctypes.c_int),
-        ("reserved", ctypes.c_int),
+        ("search_variant", ctypes.c_int),
         ("c_puct", ctypes.c_double),
         ("discount", ctypes.c_double),
         ("dirichlet_alpha", ctypes.c_double),

@@ -25,6 +25,7 @@ class EngineConfig:
     max_moves: int = 0            # 0 = N*N (self_play.py:461)
     compat: str = "reference"     # "reference" (zero visit counts, §0.6) or "fixed"
     temperature_moves: int = 15
+    search_variant: str = "self_play"   # "self_play" (self_play.py MCTS) or "main" (main.py:246-368)
     c_puct: float = 2.5
     discount: float = 0.99
     dirichlet_alpha: float = 0.15
@@ -45,6 +46,10 @@ class EngineConfig:
                 if v not in ("reference", "fixed"):
                     raise ValueError(f"compat must be 'reference' or 'fixed', not {v!r}")
                 v = 0 if v == "reference" else 1
+            if f.name == "search_variant":
+                if v not in ("self_play", "main"):
+                    raise ValueError(f"search_variant must be 'self_play' or 'main', not {v!r}")
+                v = 0 if v == "self_play" else 1
             setattr(c, f.name, v)
         return c
 

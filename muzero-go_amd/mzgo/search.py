@@ -93,6 +93,30 @@ class MCTS:
         return root, visit_counts, float(value[0].item())
 
 
+class MainMCTS:
+    """main.py's MCTS (main.py:246-368; the trainer's self-play and the arena
+    evaluator) on the device search: ``MainMCTS(net, A, S, c_puct=2).run(obs)
+    -> root``.  Defaults are main.py's Config (:37-52): Dirichlet(0.03) with
+    epsilon 0.25, pass prior 0.05, discount 0.99."""
+
+    def __init__(self, muzero_net, action_size, num_simulations, c_puct=2, *, seed=1234, game=0,
+                 dirichlet_alpha=0.03, dirichlet_epsilon=0.25, discount=0.99, pass_epsilon=0.05):
+        self._m = MCTS(muzero_net, action_size, num_simulations, c_puct, compat="fixed", seed=seed, game=game,
+                       dirichlet_alpha=dirichlet_alpha, dirichlet_epsilon=dirichlet_epsilon,
+                       discount=discount, pass_epsilon=pass_epsilon)
+        self._m.cfg["search_variant"] = "main"
+        self.net, self.action_size, self.num_simulations = muzero_net, action_size, num_simulations
+
+    @property
+    def root_child_visits(self):
+        return self._m.root_child_visits
+
+    def run(self, observation, move_index=0, noise=None):
+        root, _visits, value = self._m.run(observation, move_index=move_index, noise=noise)
+        self.root_value = value
+        return root
+
+
 def valid_mask_of(observation, pass_epsilon=0.01):
     """valid_mask of self_play.py:363-370 (float64, pass last)."""
     valid_board = (np.asarray(observation)[3].flatten() == 0).astype(np.float32)

@@ -117,3 +117,27 @@ def test_search_matches_oracle_tree(N, S, moves):
     np.testing.assert_array_equal(visits, r_visits)
     np.testing.assert_array_equal(np.array(depth), np.array(r_depth))
     assert abs(value - r_value) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["5x5_s25_mid", "9x9_s200_empty", "9x9_s200_mid"])
+def test_main_variant_search_matches_reference_tree(golden_dir, case):
+    """search_variant="main": main.py's MCTS (main.py:246-368) on the device vs
+    trees recorded from the reference main.py under the same hooks."""
+    import mzgo
+    from oracle.mcts import tree_summary
+    from oracle.rng import injected_noise
+    g = np.load(f"{golden_dir}/mctsmain_{case}.npz")
+    N, S = int(g["N"]), int(g["S"])
+    seed, game, move = int(g["seed"]), int(g["game"]), int(g["move"])
+    A = N * N + 1
+    m = mzgo.MainMCTS(_net(N), A, S, c_puct=float(g["c_puct"]), seed=seed, game=game,
+                      dirichlet_epsilon=float(g["dirichlet_epsilon"]), pass_epsilon=float(g["pass_epsilon"]),
+                      discount=float(g["discount"]))
+    root = m.run(g["obs"], move_index=move, noise=torch.from_numpy(injected_noise(seed, game, move, A)))
+    assert root.visit_count == int(g["root_n"])
+    np.testing.assert_allclose([root.children[a]["prior"] for a in range(A)], g["root_priors"],
+                               rtol=1e-5, atol=1e-9)
+    visits, depth = tree_summary(root, A)
+    np.testing.assert_array_equal(visits, g["visits"])
+    np.testing.assert_array_equal(np.array(depth), g["depth_hist"])
+    assert abs(m.root_value - float(g["root_value"])) < 1e-5

@@ -113,3 +113,23 @@ def test_records_pack_matches_export():
         assert got["length"] == want["length"] == 9
         for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
             np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+
+
+def test_main_variant_games_follow_main_move_rule():
+    """search_variant="main" (main.py:246-368 search + the :660-673 move rule):
+    legal moves on the oracle board, policy = child visits / sum over valid
+    actions, action = first argmax of those visits."""
+    import mzgo
+    N, G, S = 9, 16, 24
+    sp = mzgo.SelfPlay(_net(N), G, S, seed=5, search_variant="main", c_puct=2.0, dirichlet_alpha=0.03,
+                       dirichlet_epsilon=0.25, pass_epsilon=0.05)
+    hists = sp.play()
+    for h in hists:
+        st = gg.init_state(N)
+        for obs, a, pol in zip(h.observations, h.actions, h.policies):
+            np.testing.assert_array_equal(obs, st)
+            mask = root_valid_mask(obs, 0.05)
+            assert mask[a] > 0
+            assert abs(pol.sum() - 1.0) < 1e-12 and np.all(pol[mask == 0] == 0)
+            assert int(np.argmax(pol)) == a
+            st = gg.next_state(st, a)
