@@ -131,6 +131,15 @@ int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uin
  * [3] slots still playing now. */
 int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
+
+/* Arena (main.py:526-611, SelfPlayEvaluator): like mzgo_selfplay_move, but
+ * game i (global id) is played between two networks -- eng's ("current",
+ * turn 0) and opponent's ("best", turn 1); game i's first mover is turn
+ * i % 2 and turns alternate.  Search, move rule and records are eng's
+ * (use search_variant 1 for main.py's rules); opponent only lends its
+ * weights (same board_size and latent_dim).  Replaces the evaluator's
+ * MCTS(current/best net).run + argmax loop (main.py:548-568). */
+int mzgo_arena_move(mzgo_engine* eng, mzgo_engine* opponent, void* stream);
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
 /* Test hook: use injected Dirichlet samples f64 [G][max_moves][A] (device,
  * caller-owned, must outlive the moves) instead of the counter-RNG sampler;

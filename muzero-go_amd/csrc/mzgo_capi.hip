@@ -14,10 +14,11 @@
 #include "mzgo_dispatch.hpp"
 
 namespace mzgo {
-extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96;
+extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96, kernels_n6_c128;
 
 const KernelSet* find_kernels(int N, int C) {
-  static const KernelSet* all[] = {&kernels_n5_c96, &kernels_n6_c96, &kernels_n9_c96, &kernels_n19_c96};
+  static const KernelSet* all[] = {&kernels_n5_c96, &kernels_n6_c96, &kernels_n9_c96, &kernels_n19_c96,
+                                   &kernels_n6_c128};
   for (const KernelSet* k : all)
     if (k->N == N && k->C == C) return k;
   return nullptr;
@@ -272,7 +273,7 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   *out = nullptr;
   const int N = cfg->board_size, C = cfg->latent_dim;
   const KernelSet* ks = find_kernels(N, C == 0 ? 96 : C);
-  if (!ks) return fail(MZGO_EINVAL, "unsupported board_size %d / latent_dim %d (built: N in {5,6,9,19}, C=96)", N, C);
+  if (!ks) return fail(MZGO_EINVAL, "unsupported board_size %d / latent_dim %d (built: N in {5,6,9,19} with C=96; N=6 with C=128)", N, C);
   if (cfg->num_games < 1) return fail(MZGO_EINVAL, "num_games must be >= 1");
   if (C != 0 && cfg->num_simulations < 1) return fail(MZGO_EINVAL, "num_simulations must be >= 1");
   if (cfg->compat != 0 && cfg->compat != 1) return fail(MZGO_EINVAL, "compat must be 0 or 1");
@@ -476,7 +477,29 @@ int mzgo_selfplay_move(mzgo_engine* e, void* stream) {
   pp.game_base = e->cfg.game_base;
   pp.epoch = e->epoch;
   pp.noise = e->noise;
-  HIPCHK(e->ks->selfplay_move(e->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  pp.arena = 0;
+  HIPCHK(e->ks->selfplay_move(e->np, e->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_arena_move(mzgo_engine* e, mzgo_engine* opponent, void* stream) {
+  if (!e || !opponent || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  if (opponent->N != e->N || opponent->C != e->C)
+    return fail(MZGO_EINVAL, "arena engines differ in board size / latent_dim (%d/%d vs %d/%d)", e->N, e->C,
+                opponent->N, opponent->C);
+  int rc = e->sync_weights();
+  if (rc) return rc;
+  rc = opponent->sync_weights();
+  if (rc) return rc;
+  PlayParams pp;
+  pp.temperature = e->cfg.temperature;
+  pp.temperature_moves = e->cfg.temperature_moves;
+  pp.komi = e->cfg.komi;
+  pp.game_base = e->cfg.game_base;
+  pp.epoch = e->epoch;
+  pp.noise = e->noise;
+  pp.arena = 1;
+  HIPCHK(e->ks->selfplay_move(e->np, opponent->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
 

@@ -585,11 +585,13 @@ struct PlayParams {
   int game_base;          // global id of slot 0 (multi-GPU sharding)
   int epoch;              // game generation (slot restarts), part of the RNG key
   const double* noise;    // test hook: injected Dirichlet samples [G][M][A], or null
+  int arena;              // 0: one network; 1: main.py's evaluator -- game i's first
+                          // mover is network (i % 2), then the networks alternate
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np, SearchParams sp, PlayParams pp,
-                                                             EngineArrays E) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np_a, NetParams np_b, SearchParams sp,
+                                                             PlayParams pp, EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
@@ -598,6 +600,9 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   BoardMeta m;
   load_board<G>(sm, E, g, m);
   const int mv = m.moves;
+  // arena (main.py:535-549): turn 0 = "current" (np_a), 1 = "best" (np_b); game
+  // i starts with turn i % 2 (evaluate, :597-599)
+  const NetParams& np = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? np_b : np_a;
   const size_t rec = (size_t)g * E.max_moves + mv;
   for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     E.rec_stones[rec * G::CELLS + c] = sm.stone[c];

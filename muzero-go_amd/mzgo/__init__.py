@@ -8,8 +8,10 @@ self_play.py), all executed by libmzgo.so's HIP kernels:
 * ``MainMCTS`` -- main.py's MCTS variant (trainer self-play / arena) on the same kernels
 * ``GoEnv``       -- GymGo rules as bit-exact integer kernels
 * ``SelfPlay``    -- G concurrent games per GPU, one fused kernel step per move
+* ``SelfPlayEvaluator`` -- main.py's arena (two networks, all games at once)
 * ``GameHistory``, ``save_batches`` -- the reference's record / pickle format
 """
+from .arena import SelfPlayEvaluator
 from .engine import Engine, EngineConfig
 from .env import GoEnv
 from .net import MuZeroNet
@@ -18,4 +20,4 @@ from .selfplay import GameHistory, SelfPlay, history_from_device, save_batches
 from .weights import deterministic_state_dict
 
 __all__ = ["Engine", "EngineConfig", "GoEnv", "MuZeroNet", "MCTS", "MainMCTS", "MuZeroAgent", "SelfPlay",
-           "GameHistory", "history_from_device", "save_batches", "deterministic_state_dict"]
+           "GameHistory", "history_from_device", "save_batches", "deterministic_state_dict", "SelfPlayEvaluator"]

@@ -189,6 +189,11 @@ class Engine:
     def selfplay_move(self):
         check(lib.mzgo_selfplay_move(self._h, stream_of(self.device)))
 
+    def arena_move(self, opponent):
+        """One move of every unfinished arena game: this engine's network plays
+        turn 0, ``opponent``'s turn 1 (mzgo_arena_move)."""
+        check(lib.mzgo_arena_move(self._h, opponent.handle, stream_of(self.device)))
+
     def inject_noise(self, noise):
         """Test hook: Dirichlet samples float64 [G, max_moves, A] on the GPU (None = sample)."""
         if noise is not None:

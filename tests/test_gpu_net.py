@@ -44,14 +44,15 @@ def test_inference_matches_reference_golden(golden_dir, N):
         assert e_gpu <= 4 * e_ref + 1e-6, f"{k}: gpu err {e_gpu} vs torch-fp32 err {e_ref}"
 
 
-@pytest.mark.parametrize("N,B", [(5, 33), (6, 7), (9, 256), (19, 9)])
-def test_batched_inference_matches_oracle(N, B):
+@pytest.mark.parametrize("N,B,C", [(5, 33, 96), (6, 7, 96), (9, 256, 96), (19, 9, 96), (6, 16, 128)])
+def test_batched_inference_matches_oracle(N, B, C):
+    """C=128 at 6x6 is main.py's training configuration (main.py:27-30)."""
     from oracle.net import OracleNet
-    net, sd = _net(N, seed=3)
+    net, sd = _net(N, seed=3, C=C)
     ref = OracleNet(sd)
     gen = torch.Generator().manual_seed(N * 100 + B)
     obs = (torch.rand(B, 6, N, N, generator=gen) < 0.3).float()
-    lat_in = torch.rand(B, 96, N, N, generator=gen) * 2
+    lat_in = torch.rand(B, C, N, N, generator=gen) * 2
     act = torch.randint(0, N * N + 1, (B,), generator=gen)
     lat, v0, lg0 = net.initial_inference(obs.cuda())
     nl, r1, v1, lg1 = net.recurrent_inference(lat_in.cuda(), act.cuda())

@@ -141,3 +141,34 @@ def test_main_variant_search_matches_reference_tree(golden_dir, case):
     np.testing.assert_array_equal(visits, g["visits"])
     np.testing.assert_array_equal(np.array(depth), g["depth_hist"])
     assert abs(m.root_value - float(g["root_value"])) < 1e-5
+
+
+@pytest.mark.parametrize("moves", [0, 8])
+def test_main_variant_6x6_c128_matches_oracle(moves):
+    """main.py's own configuration (6x6, latent_dim 128, main.py:27-53): the
+    device main-variant tree vs oracle.mcts_main (pinned by the main.py
+    goldens above) on the same hooks."""
+    import mzgo
+    from oracle.mcts import tree_summary
+    from oracle.mcts_main import MCTSMain
+    from oracle.net import OracleNet
+    from oracle.positions import random_position
+    from oracle.rng import SearchHooks, injected_noise
+    from oracle.weights import deterministic_state_dict
+    N, C, S, seed, game, move = 6, 128, 96, 17, 1, moves
+    A = N * N + 1
+    obs = random_position(N, moves, 300 + moves) if moves else np.zeros((6, N, N))
+    noise = injected_noise(seed, game, move, A)
+    hooks = SearchHooks(seed, game, move)
+    sd = deterministic_state_dict(C, A, 0)
+    ref = MCTSMain(OracleNet(sd), A, S, choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+                   noise=lambda p, a, e: (1 - e) * p + e * noise)
+    with torch.no_grad():
+        r_root = ref.run(obs)
+    net = mzgo.MuZeroNet(C, A).to("cuda").eval()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = mzgo.MainMCTS(net, A, S, seed=seed, game=game)
+    root = m.run(obs, move_index=move, noise=torch.from_numpy(noise))
+    np.testing.assert_array_equal(tree_summary(root, A)[0], tree_summary(r_root, A)[0])
+    np.testing.assert_array_equal(np.array(tree_summary(root, A)[1]), np.array(tree_summary(r_root, A)[1]))
+    assert abs(m.root_value - r_root.value()) < 1e-5
