@@ -154,6 +154,8 @@ struct mzgo_engine {
   NetParams np{};
   EngineArrays E{};
   int* d_err = nullptr;
+  float* d_scr = nullptr;      // initial_inference scratch (strip boards), grown on demand
+  size_t scr_floats = 0;
   std::vector<void*> allocs;
   int64_t bytes = 0;
   int epoch = 0;
@@ -172,6 +174,7 @@ struct mzgo_engine {
   ~mzgo_engine() {
     for (void* p : allocs) (void)hipFree(p);
     if (d_w) (void)hipFree(d_w);
+    if (d_scr) (void)hipFree(d_scr);
   }
 
   // pack + upload the network if any tensor changed since the last upload
@@ -186,7 +189,7 @@ struct mzgo_engine {
     // k-range split of the ring conv: 2 when the board runs 8 waves (Geo::KSPLIT)
     const int ct = (N * N + 15) / 16, ng = ct >= 3 ? 3 : ct, ncg = (ct + ng - 1) / ng;
     const int ksplit = ncg <= 2 ? 2 : 1;
-    const bool wino = N == 9;                      // Geo::WINO
+    const bool wino = N == 9 || N == 19;           // Geo::WINO
     auto latent = [&](const char* key, int cout, int cin) {
       return wino ? pack_wino(sd[key].data(), cout, cin) : pack_conv(sd[key].data(), cout, cin, true, ksplit);
     };
@@ -374,7 +377,19 @@ int mzgo_initial_inference(mzgo_engine* e, const float* obs, int B, float* laten
   if (!e || !obs || !latent || !value || !logits || B < 1) return fail(MZGO_EINVAL, "bad argument");
   int rc = e->sync_weights();
   if (rc) return rc;
-  HIPCHK(e->ks->initial_inference(e->np, obs, B, latent, value, logits, (hipStream_t)stream));
+  float* scr = nullptr;
+  if (e->ks->rep_scratch) {
+    const size_t need = (size_t)B * e->ks->rep_scratch;
+    if (need > e->scr_floats) {
+      if (e->d_scr) HIPCHK(hipFree(e->d_scr));   // synchronising: no launch still reads it
+      e->d_scr = nullptr;
+      e->scr_floats = 0;
+      HIPCHK(hipMalloc(&e->d_scr, need * sizeof(float)));
+      e->scr_floats = need;
+    }
+    scr = e->d_scr;
+  }
+  HIPCHK(e->ks->initial_inference(e->np, obs, B, latent, value, logits, scr, (hipStream_t)stream));
   return MZGO_OK;
 }
 

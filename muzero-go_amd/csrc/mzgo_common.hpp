@@ -35,7 +35,7 @@ struct Geo {
   static constexpr int NCG = (CT + NG - 1) / NG;  // cell groups
   static constexpr int AP = (A + 63) / 64;        // actions per lane (a = lane + 64*j)
   // 9x9 runs its latent convs as Winograd F(2,3)xF(3,3) GEMMs (mzgo_wino.hpp)
-  static constexpr bool WINO = N == 9;
+  static constexpr bool WINO = N == 9 || N == 19;
   static constexpr int WAVES = WINO ? 12 : (NCG <= 2 ? 8 : 4);  // waves per workgroup
   static constexpr int THREADS = WAVES * 64;
   static constexpr int WPE = WAVES / 4;           // waves per SIMD

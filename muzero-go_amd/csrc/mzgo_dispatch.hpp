@@ -8,8 +8,9 @@ namespace mzgo {
 struct KernelSet {
   int N, C;
   size_t lds_bytes;
+  int rep_scratch;   // floats of HBM scratch per initial_inference item (strip boards), else 0
   hipError_t (*initial_inference)(const NetParams&, const float* obs, int B, float* lat, float* val,
-                                  float* logits, hipStream_t);
+                                  float* logits, float* scratch, hipStream_t);
   hipError_t (*recurrent_inference)(const NetParams&, const float* lat, const int64_t* act, int B,
                                     float* nlat, float* rew, float* val, float* logits, int* err,
                                     hipStream_t);
@@ -29,8 +30,9 @@ const KernelSet* find_kernels(int N, int C);
 template <int N, int C>
 struct Launch {
   static hipError_t ii(const NetParams& np, const float* obs, int B, float* lat, float* val,
-                       float* logits, hipStream_t s) {
-    hipLaunchKernelGGL((k_initial_inference<N, C>), dim3(B), dim3(Geo<N, C>::THREADS), 0, s, np, obs, lat, val, logits);
+                       float* logits, float* scratch, hipStream_t s) {
+    hipLaunchKernelGGL((k_initial_inference<N, C>), dim3(B), dim3(Geo<N, C>::THREADS), 0, s, np, obs, lat, val, logits,
+                       scratch);
     return hipGetLastError();
   }
   static hipError_t ri(const NetParams& np, const float* lat, const int64_t* act, int B, float* nlat,
@@ -65,7 +67,7 @@ struct Launch {
     return hipGetLastError();
   }
   static KernelSet table() {
-    return KernelSet{N, C, sizeof(Smem<Geo<N, C>>), &ii, &ri, &search, &breset, &bstep, &bplanes, &move};
+    return KernelSet{N, C, sizeof(Smem<Geo<N, C>>), rep_needs_scratch<Geo<N, C>>() ? 64 * N * N : 0, &ii, &ri, &search, &breset, &bstep, &bplanes, &move};
   }
 };
 

@@ -96,20 +96,22 @@ struct Smem<G, true> {
     float v[Wino<G>::template v_floats<G::CINMAX>()];    // transformed conv input
     struct {
       float red[Wino<G>::template red_floats<G::C>()];
-      float hp[(G::C / 16) * 3 * G::CS];
+      float hp[(G::C / 16) * 3 * Wino<G>::HS];   // head partials of one strip
       alignas(16) float outs[G::C * Wino<G>::OUT_STRIDE];   // conv output staging
     } x;
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
   } u;
   alignas(16) float raw[WinoRaw<G>::FLOATS];              // per-wave staging of conv input rows
+  static constexpr bool STRIPS = Wino<G>::NSTRIP > 1;
+  alignas(16) float hfin[STRIPS ? 3 * G::CS : 4];         // strip boards: summed head partials
   TreeLds<G> t;
   int8_t stone[G::CELLS];
   uint8_t invd[G::CELLS];
   int killed[4];
   int misc[8];
   int bc[8];
-  __device__ float* heads() { return u.x.hp; }
-  static constexpr int HEAD_PARTS = G::C / 16;
+  __device__ float* heads() { return STRIPS ? hfin : u.x.hp; }
+  static constexpr int HEAD_PARTS = STRIPS ? 1 : G::C / 16;
 };
 
 // One latent conv: src ([CIN][src_stride], global) (+ emb per channel) ->
@@ -121,10 +123,15 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
                                             int dst_stride, int out_cells, const float* head_w,
                                             Stamp* st = nullptr) {
   if constexpr (G::WINO) {
-    wino_input<G, CIN>(sm.u.v, sm.raw, src, src_stride, emb, st);
-    if (st) st->lap(1);
-    wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, w, b, dst, dst_stride, out_cells,
-                                head_w, st);
+    // row strips (19x19): strip s reads rows s*SROWS-1 .. (s+1)*SROWS of src,
+    // so src must not alias dst (representation ping-pongs through scratch)
+    for (int s = 0; s < Wino<G>::NSTRIP; ++s) {
+      wino_input<G, CIN>(sm.u.v, sm.raw, src, src_stride, emb, s, st);
+      if (st) st->lap(1);
+      wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, w, b, dst, dst_stride,
+                                  out_cells, head_w, s, st);
+    }
+    if constexpr (Wino<G>::NSTRIP > 1) __syncthreads();   // hfin complete
   } else {
     stage_board<G>(sm.u.in, src, src_stride, CIN, emb);
     __syncthreads();
@@ -145,12 +152,21 @@ __device__ __forceinline__ BoardLds<G> board_lds(Smem<G>& sm) {
 // ---------------------------------------------------------------------------
 // representation (self_play.py:70-74) + prediction heads (:104-113).
 // planes(c, cell) gives the f32 observation.  The latent is written to
-// ``lat`` ([C][lat_stride]), which also serves as scratch for conv1/conv2.
+// ``lat`` ([C][lat_stride]), which also serves as scratch for conv1/conv2;
+// strip boards put conv2's output in ``scr`` ([64][lat_stride]) instead (a
+// strip conv cannot run in place).
 // Leaves the logits in sm.t.logits and the value in sm.t.value.
 // ---------------------------------------------------------------------------
+template <class G>
+constexpr bool rep_needs_scratch() {
+  if constexpr (G::WINO) return Wino<G>::NSTRIP > 1;
+  else return false;
+}
+
 template <class G, class PlaneFn>
 __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
-                                      int lat_stride) {
+                                      int lat_stride, float* scr) {
+  float* mid = rep_needs_scratch<G>() ? scr : lat;
   for (int i = threadIdx.x; i < 6 * G::CELLS; i += G::THREADS) {
     const int c = i / G::CELLS, j = i - c * G::CELLS;
     sm.u.in[c * G::CPAD + j] = planes(c, j);
@@ -162,9 +178,9 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
   const int oc = lat_stride == G::CS ? G::CS : G::CELLS;   // pooled latents also write their 0 pads
   conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
   __syncthreads();
-  latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, lat, lat_stride, oc, nullptr);
+  latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, mid, lat_stride, oc, nullptr);
   __syncthreads();                                         // conv2's stores before conv3 reads them
-  latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, lat, lat_stride, nullptr, lat, lat_stride, oc,
+  latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, mid, lat_stride, nullptr, lat, lat_stride, oc,
                               np.head_w + G::C);
   if (wave_id() == 0)
     finalize_heads<G, Smem<G>::HEAD_PARTS>(sm.heads(), false, sm.t.hsc, sm.t.logits, &sm.t.reward, &sm.t.value);
@@ -189,14 +205,16 @@ __device__ __forceinline__ void dynamics(Smem<G>& sm, const NetParams& np, const
 // ---------------------------------------------------------------------------
 template <int N, int C>
 __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_initial_inference(NetParams np, const float* __restrict__ obs,
-                                                                 float* latent, float* value, float* logits) {
+                                                                 float* latent, float* value, float* logits,
+                                                                 float* scratch) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int b = blockIdx.x;
   const float* o = obs + (size_t)b * 6 * G::CELLS;
   float* lat = latent + (size_t)b * G::C * G::CELLS;
-  representation<G>(sm, np, [&](int c, int j) { return o[c * G::CELLS + j]; }, lat, G::CELLS);
+  float* scr = scratch ? scratch + (size_t)b * 64 * G::CELLS : nullptr;
+  representation<G>(sm, np, [&](int c, int j) { return o[c * G::CELLS + j]; }, lat, G::CELLS, scr);
   for (int a = threadIdx.x; a < G::A; a += G::THREADS) logits[(size_t)b * G::A + a] = sm.t.logits[a];
   if (threadIdx.x == 0) value[b] = sm.t.value;
 }
@@ -289,8 +307,9 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
                                   uint64_t key) {
   const TreeView TV = TreeViewOf<G>::make(E, g);
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
-  representation<G>(sm, np, planes, E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS,
-                    G::CS);                              // root latent -> node 0
+  float* root = E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS;
+  representation<G>(sm, np, planes, root, G::CS,
+                    root + (size_t)G::C * G::CS);        // root latent -> node 0 (node 1's slot: scratch)
   if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
   __syncthreads();
   if constexpr (G::TREE_CAP > 0) {

@@ -1,4 +1,4 @@
-// mzgo_wino.hpp -- the 3x3/pad-1 convolution of one 9x9 board as a Winograd
+// mzgo_wino.hpp -- the 3x3/pad-1 convolution of one board as a Winograd
 // F(2,3) x F(3,3) transform on fp32 MFMA (v_mfma_f32_16x16x4_f32), with the
 // MuZero heads fused into the epilogue.
 //
@@ -18,6 +18,9 @@
 // L2 into VGPRs -- nothing but the transformed input lives in LDS.  The two
 // xi halves exchange half of their transformed outputs through LDS: wave h
 // finalises output row oy = h of each tile.
+//
+// 19x19 (10 x 7 = 70 tiles) runs the same GEMM over 5 row strips of 2 tile
+// rows (14 tiles each): 5 x 2880 MFMAs per conv instead of 29808 direct.
 //
 // Replaces the torch conv2d calls of self_play.py:72-74 (representation
 // conv2/conv3), :90 (dynamics) and the 1x1 head convs of :81, :100, :102.
@@ -50,17 +53,27 @@ template <class G>
 struct Wino {
   static constexpr int TY = (G::N + 1) / 2;   // F(2,3) tiles along rows
   static constexpr int TX = (G::N + 2) / 3;   // F(3,3) tiles along columns
-  static constexpr int T = TY * TX;           // tiles (MFMA columns)
+  static constexpr int TRS = (16 / TX < TY) ? 16 / TX : TY;   // tile rows per strip
+  static constexpr int NSTRIP = (TY + TRS - 1) / TRS;          // strips (9x9: 1, 19x19: 5)
+  static constexpr int T = TRS * TX;          // tiles per strip (MFMA columns)
+  static constexpr int SROWS = 2 * TRS;       // output rows per strip
+  static constexpr int SCELLS = SROWS * G::N; // output cells per strip (incl. rows >= N)
   static constexpr int XI = 20;               // 4 x 5 transform points
-  static_assert(T <= 16, "tiles must fit one MFMA column tile");
+  static_assert(T <= 16, "a strip's tiles must fit one MFMA column tile");
+  // cells of a staged output row: a strip's cells; the last strip also carries
+  // the pooled layout's pad cells up to CS
+  static constexpr int LAST_C0 = (NSTRIP - 1) * SCELLS;
+  static constexpr int OCELLS = SCELLS > G::CS - LAST_C0 ? SCELLS : G::CS - LAST_C0;
   // output staging row stride: 4 cout rows apart (the kq lane groups) land 16
-  // banks apart instead of on the same bank
-  static constexpr int OUT_STRIDE = G::CS + (36 - G::CS % 32) % 32;
-  static_assert(OUT_STRIDE > G::CS, "junk cell CS past the stored row");
+  // banks apart; one junk cell (OCELLS) past the stored cells
+  static constexpr int OUT_STRIDE = OCELLS + (36 - OCELLS % 32) % 32;
+  static_assert(OUT_STRIDE > OCELLS, "junk cell past the stored row");
+  // head partials [m][3][HS] per strip (one strip: the whole pooled row)
+  static constexpr int HS = NSTRIP == 1 ? G::CS : OCELLS;
   // V floats for CIN input channels: [xi][h][s4][kq][t16][e4]
   template <int CIN>
   static constexpr int v_floats() { return XI * CIN * 16; }
-  // exchange buffer [m][h][ox*4 + r][lane] + head partials [m][3][CS]
+  // exchange buffer [m][h][ox*4 + r][lane]
   template <int COUT>
   static constexpr int red_floats() { return (COUT / 16) * 2 * 12 * 64; }
 };
@@ -73,26 +86,61 @@ struct Wino {
 //
 // Work unit: a channel quad (h, s4, kq) = the 4 channels e = 0..3 that share
 // one V row; lane (t, e) transforms tile t of channel e.  Each wave fetches
-// its quads' rows itself (coalesced 16-byte loads, all in flight at once) and
-// scatters them, embedding already added, into its own slice of raw: one
-// zero-haloed (N+3) x (N+2) plane per channel (rows -1..N+1, cols -1..N), so
-// every tap of every tile is a plain load at a constant offset -- no bounds
+// its quads' rows itself (all loads in flight at once) and scatters them,
+// embedding already added, into its own slice of raw: one zero-haloed plane
+// per channel covering the strip's rows -1..SROWS and columns -1..N, so every
+// tap of every tile is a plain load at a constant offset -- no bounds
 // selects.  The only workgroup barrier is the one before the GEMM.
 template <class G>
 struct WinoRaw {
-  static_assert(G::N == 9, "bank layout derived for 9x9 tiles");
+  static_assert(G::N == 9 || G::N == 19, "bank layout derived for 9x9 and 19x19 tiles");
   static constexpr int PW = G::N + 2;                    // padded width
-  static constexpr int PH = 2 * Wino<G>::TY + 2;         // padded height (last tile row + halo)
+  static constexpr int PH = Wino<G>::SROWS + 2;          // padded height (strip rows + halo)
   static constexpr int PLANE = PH * PW;
-  // plane stride == 11 (mod 32): lanes of channels e and e+1 (one 32-lane
-  // half) then share only 2 of their 15 tile banks (offsets 22*ty + 3*tx)
+  // plane stride == 11 (mod 32): the lanes of channels e and e+1 (one 32-lane
+  // half) share 2 of 15 tile banks at 9x9 (offsets 22*ty + 3*tx) and none at
+  // 19x19 (42*ty + 3*tx)
   static constexpr int STRIDE = PLANE + ((11 - PLANE % 32) % 32 + 32) % 32;
   static_assert(STRIDE > PLANE, "a junk slot past each plane");
   static constexpr int FLOATS = G::WAVES * 4 * STRIDE;   // all waves' slices
 };
 
-// The halo of every raw plane must be 0 before the first wino_input of a
-// kernel (it is never written afterwards).  All threads; synchronises.
+// The 4 x 5 patch of tile (ty, tx) of channel e (plane my + e*RS) -> the 20
+// V entries of that (channel, tile): BT2 along rows, then BT3 along columns.
+template <class G, int CIN>
+__device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const float* my, int quad, int t,
+                                                    int e, int ty, int tx) {
+  constexpr int S4 = CIN / 32, PW = WinoRaw<G>::PW, RS = WinoRaw<G>::STRIDE;
+  const float* s = my + e * RS + (2 * ty) * PW + 3 * tx;   // tile's top-left (padded coords)
+  float d[4][5];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) d[a][b] = s[a * PW + b];
+  float u[4][5];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {               // BT2 along rows
+    u[0][b] = d[0][b] - d[2][b];
+    u[1][b] = d[1][b] + d[2][b];
+    u[2][b] = d[2][b] - d[1][b];
+    u[3][b] = d[3][b] - d[1][b];
+  }
+  float* vb = V + (size_t)quad * 64 + t * 4 + e;         // quad index == (h*S4 + s4)*4 + kq
+  constexpr int XSTRIDE = 2 * S4 * 4 * 64;    // floats between xi planes
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {               // BT3 along columns
+    const float* q = u[i];
+    vb[(i * 5 + 0) * XSTRIDE] = ((2.f * q[0] + q[1]) - 2.f * q[2]) - q[3];
+    vb[(i * 5 + 1) * XSTRIDE] = (2.f * q[1] + 3.f * q[2]) + q[3];
+    vb[(i * 5 + 2) * XSTRIDE] = (q[2] - 2.f * q[1]) + q[3];
+    vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
+    vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
+  }
+}
+
+// The halo columns of every raw plane must be 0 before the first wino_input
+// of a kernel (never written afterwards; halo rows are rewritten per strip).
+// All threads; synchronises.
 template <class G>
 __device__ __forceinline__ void wino_raw_zero(float* raw) {
   for (int i = threadIdx.x; i < WinoRaw<G>::FLOATS; i += G::THREADS) raw[i] = 0.f;
@@ -102,101 +150,112 @@ __device__ __forceinline__ void wino_raw_zero(float* raw) {
 template <class G, int CIN>
 __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restrict__ raw,
                                            const float* __restrict__ src, int src_stride,
-                                           const float* __restrict__ emb, Stamp* st = nullptr) {
+                                           const float* __restrict__ emb, int strip = 0,
+                                           Stamp* st = nullptr) {
   typedef Wino<G> W;
   typedef WinoRaw<G> R;
-  constexpr int CH = CIN / 2, S4 = CH / 16, RS = R::STRIDE, PW = R::PW;
+  constexpr int CH = CIN / 2, S4 = CH / 16, RS = R::STRIDE, PW = R::PW, PH = R::PH;
   static_assert(CIN % 32 == 0, "two cin halves of whole 4-k-step groups");
   constexpr int QUADS = 2 * S4 * 4;           // (h, s4, kq)
   constexpr int QPW = (QUADS + G::WAVES - 1) / G::WAVES;   // quads per wave
+  // whole pooled rows (one strip: 16-byte loads of all CS cells) or, per
+  // strip, the strip's PH rows of N cells (4-byte loads, any stride)
+  const bool fast = W::NSTRIP == 1 && src_stride == G::CS;
   constexpr int Q4 = G::CS / 4;               // float4 per pooled channel row
-  constexpr int NQ = 4 * Q4;                  // float4 per quad
-  constexpr int PER = (NQ + 63) / 64;         // float4 loads per lane per quad
+  constexpr int NQ = 4 * Q4;                  // float4 per quad (fast path)
+  constexpr int PER = (NQ + 63) / 64;
+  constexpr int NE = 4 * PH * G::N;           // floats per quad (strip path)
+  constexpr int PERS = (NE + 63) / 64;
   const int lane = lane_id_local();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   const int t = lane & 15, e = lane >> 4;
   const int tt = t < W::T ? t : W::T - 1;     // pad column: any valid tile (output unused)
   const int ty = tt / W::TX, tx = tt - ty * W::TX;
-  const bool pooled = src_stride == G::CS;
+  const int row0 = strip * W::SROWS - 1;      // board row of padded row 0
   float* my = raw + wave * 4 * RS;
   auto chan = [&](int quad, int ee) {         // channel of quad member ee
     const int h = quad / (S4 * 4), s4 = (quad / 4) % S4, kq = quad % 4;
     return h * CH + 4 * (4 * s4 + ee) + kq;
   };
-  auto pidx = [&](int cell) { const int y = cell / G::N; return (y + 1) * PW + (cell - y * G::N) + 1; };
-
-  // all of this wave's rows (and their embedding values) in flight at once;
-  // loads are branch-free (clamped indices) so they stay outstanding together
-  f32x4 rg[QPW][PER];
-  float eg[QPW][PER];
-  const f32x4* s4p = reinterpret_cast<const f32x4*>(src);
+  auto pidx = [&](int cell) { const int y = cell / G::N; return (y - row0) * PW + (cell - y * G::N) + 1; };
   const float* ebase = emb ? emb : src;
+
+  if (strip > 0) __syncthreads();            // the previous strip's epilogue is done with LDS
+  if (fast) {
+    // all of this wave's rows (and their embedding values) in flight at once;
+    // loads are branch-free (clamped indices) so they stay outstanding together
+    f32x4 rg[QPW][PER];
+    float eg[QPW][PER];
+    const f32x4* s4p = reinterpret_cast<const f32x4*>(src);
 #pragma unroll
-  for (int k = 0; k < QPW; ++k) {
-    const int quad = min(wave + k * G::WAVES, QUADS - 1);
+    for (int k = 0; k < QPW; ++k) {
+      const int quad = min(wave + k * G::WAVES, QUADS - 1);
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int i = min(lane + 64 * p, NQ - 1);
+        rg[k][p] = s4p[chan(quad, i / Q4) * Q4 + i % Q4];
+        eg[k][p] = ebase[chan(quad, i / Q4)];
+      }
+    }
+    if (st) st->lap(20);
+    // scatter targets of this lane's 4*PER floats (pad cells and surplus lanes
+    // go to a junk slot past the plane): the same for every quad
+    int widx[PER][4];
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
-      const int i = min(lane + 64 * p, NQ - 1);
-      if (pooled) rg[k][p] = s4p[chan(quad, i / Q4) * Q4 + i % Q4];
-      eg[k][p] = ebase[chan(quad, i / Q4)];
+      const int i = lane + 64 * p, ee = min(i, NQ - 1) / Q4, c0 = (min(i, NQ - 1) % Q4) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        widx[p][r] = (i < NQ && c0 + r < G::CELLS) ? ee * RS + pidx(c0 + r) : R::PLANE;
     }
-  }
-  if (st) st->lap(20);
-  // scatter targets of this lane's 4*PER floats (pad cells and surplus lanes
-  // go to a junk slot past the plane): the same for every quad
-  int widx[PER][4];
 #pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const int i = lane + 64 * p, ee = min(i, NQ - 1) / Q4, c0 = (min(i, NQ - 1) % Q4) * 4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      widx[p][r] = (i < NQ && c0 + r < G::CELLS) ? ee * RS + pidx(c0 + r) : R::PLANE;
-  }
-
-#pragma unroll
-  for (int k = 0; k < QPW; ++k) {
-    const int quad = wave + k * G::WAVES;
-    if (quad >= QUADS) break;                 // wave-uniform
-    if (k) wave_lds_sync();                   // previous quad's reads are done
-    if (pooled) {
+    for (int k = 0; k < QPW; ++k) {
+      const int quad = wave + k * G::WAVES;
+      if (quad >= QUADS) break;               // wave-uniform
+      if (k) wave_lds_sync();                 // previous quad's reads are done
 #pragma unroll
       for (int p = 0; p < PER; ++p) {
         const float ec = emb ? eg[k][p] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) my[widx[p][r]] = rg[k][p][r] + ec;
       }
-    } else {
-      for (int i = lane; i < 4 * G::CELLS; i += 64) {
-        const int ee = i / G::CELLS, j = i - ee * G::CELLS;
-        const float ec = emb ? emb[chan(quad, ee)] : 0.f;
-        my[ee * RS + pidx(j)] = src[(size_t)chan(quad, ee) * src_stride + j] + ec;
+      wave_lds_sync();
+      wino_transform_quad<G, CIN>(V, my, quad, t, e, ty, tx);
+    }
+  } else {
+    // strip rows row0 .. row0+PH-1 of the quad's 4 channels (rows off the
+    // board are written as 0: the plane is reused by every strip)
+    float rv[QPW][PERS];
+#pragma unroll
+    for (int k = 0; k < QPW; ++k) {
+      const int quad = min(wave + k * G::WAVES, QUADS - 1);
+#pragma unroll
+      for (int p = 0; p < PERS; ++p) {
+        const int i = min(lane + 64 * p, NE - 1);
+        const int ee = i / (PH * G::N), r = i - ee * (PH * G::N), py = r / G::N, x = r - py * G::N;
+        const int y = row0 + py;
+        const bool on = y >= 0 && y < G::N;
+        const int c = chan(quad, ee);
+        const float v = src[(size_t)c * src_stride + (on ? y * G::N + x : 0)];
+        const float ec = emb ? ebase[c] : 0.f;
+        rv[k][p] = on ? v + ec : 0.f;
       }
     }
-    wave_lds_sync();
-    const float* s = my + e * RS + (2 * ty) * PW + 3 * tx;   // tile's top-left (padded coords)
-    float d[4][5];
+    if (st) st->lap(20);
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int k = 0; k < QPW; ++k) {
+      const int quad = wave + k * G::WAVES;
+      if (quad >= QUADS) break;               // wave-uniform
+      if (k) wave_lds_sync();
 #pragma unroll
-      for (int b = 0; b < 5; ++b) d[a][b] = s[a * PW + b];
-    float u[4][5];
-#pragma unroll
-    for (int b = 0; b < 5; ++b) {             // BT2 along rows
-      u[0][b] = d[0][b] - d[2][b];
-      u[1][b] = d[1][b] + d[2][b];
-      u[2][b] = d[2][b] - d[1][b];
-      u[3][b] = d[3][b] - d[1][b];
-    }
-    float* vb = V + (size_t)quad * 64 + t * 4 + e;       // quad index == (h*S4 + s4)*4 + kq
-    constexpr int XSTRIDE = 2 * S4 * 4 * 64;  // floats between xi planes
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {             // BT3 along columns
-      const float* q = u[i];
-      vb[(i * 5 + 0) * XSTRIDE] = ((2.f * q[0] + q[1]) - 2.f * q[2]) - q[3];
-      vb[(i * 5 + 1) * XSTRIDE] = (2.f * q[1] + 3.f * q[2]) + q[3];
-      vb[(i * 5 + 2) * XSTRIDE] = (q[2] - 2.f * q[1]) + q[3];
-      vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
-      vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
+      for (int p = 0; p < PERS; ++p) {
+        const int i = lane + 64 * p;
+        const int ee = min(i, NE - 1) / (PH * G::N), r = min(i, NE - 1) - ee * (PH * G::N);
+        const int py = r / G::N, x = r - py * G::N;
+        my[i < NE ? ee * RS + py * PW + x + 1 : R::PLANE] = rv[k][p];
+      }
+      wave_lds_sync();
+      wino_transform_quad<G, CIN>(V, my, quad, t, e, ty, tx);
     }
   }
   __syncthreads();
@@ -223,11 +282,11 @@ __device__ __forceinline__ constexpr float wino_at3(int ox, int j) {
 // global; cells >= out_cells are not stored (pooled rows, stride == out_cells
 // == CS, are stored whole with their zero pad cells).
 template <class G, int CIN, int COUT, int NH>
-__device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, float* outs,
+__device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, float* outs, float* hfin,
                                           const float* __restrict__ upk,
                                           const float* __restrict__ bias, float* __restrict__ out,
                                           int out_stride, int out_cells, const float* __restrict__ head_w,
-                                          Stamp* st = nullptr) {
+                                          int strip = 0, Stamp* st = nullptr) {
   typedef Wino<G> W;
   constexpr int CH = CIN / 2, S4 = CH / 16, MT = COUT / 16, XI = W::XI;
   constexpr int OS = W::OUT_STRIDE;
@@ -370,10 +429,11 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   }
   __syncthreads();
   if (st) st->lap(7);
+  const int c0 = strip * W::SCELLS;          // first cell of this strip
   if (active) {
     const int oy = h;
     const int ty = t / W::TX, tx = t - ty * W::TX;
-    const int y = 2 * ty + oy;
+    const int y = strip * W::SROWS + 2 * ty + oy;
     float hsum[NH > 0 ? NH : 1][3];
 #pragma unroll
     for (int hh = 0; hh < (NH > 0 ? NH : 1); ++hh)
@@ -393,7 +453,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         v = v > 0.f ? v : 0.f;
         v = valid ? v : 0.f;
         const int co = m * 16 + kq * 4 + r;
-        outs[co * OS + (valid ? cell : G::CS)] = v;  // staged (off-board lanes: junk cell CS)
+        outs[co * OS + (valid ? cell - c0 : W::OCELLS)] = v;   // staged (off-board lanes: junk cell)
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) hsum[hh][ox] = __builtin_fmaf(hw[hh][r], v, hsum[hh][ox]);
       }
@@ -407,37 +467,55 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
           v = swap_add<false>(v);               // + lane ^ 16
           v = swap_add<true>(v);                // + lane ^ 32
           const int x = 3 * tx + ox;
-          if (kq == 0 && t < W::T && y < G::N && x < G::N) hp[(m * 3 + hh) * G::CS + y * G::N + x] = v;
+          if (kq == 0 && t < W::T && y < G::N && x < G::N) hp[(m * 3 + hh) * W::HS + y * G::N + x - c0] = v;
         }
     }
   }
   // pad cells of the staged rows are 0 (the pooled layout keeps them 0)
-  for (int i = threadIdx.x; i < COUT * (G::CS - G::CELLS); i += G::THREADS) {
-    const int co = i / (G::CS - G::CELLS);
-    outs[co * OS + G::CELLS + (i - co * (G::CS - G::CELLS))] = 0.f;
-  }
+  const bool last = strip == W::NSTRIP - 1;
+  if (last)
+    for (int i = threadIdx.x; i < COUT * (G::CS - G::CELLS); i += G::THREADS) {
+      const int co = i / (G::CS - G::CELLS);
+      outs[co * OS + G::CELLS - c0 + (i - co * (G::CS - G::CELLS))] = 0.f;
+    }
   __syncthreads();
-  // whole-row stores (the tile-ordered epilogue would scatter 4-byte writes)
-  if (out != nullptr) {
-    if (out_stride == G::CS && out_cells == G::CS) {
-      constexpr int Q = G::CS / 4;
-      for (int i = threadIdx.x; i < COUT * Q; i += G::THREADS) {
-        const int co = i / Q, q = i - co * Q;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(outs + co * OS + q * 4);
-#if MZGO_NT_STORE
-        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out) + i);
-#else
-        reinterpret_cast<f32x4*>(out)[i] = v;
-#endif
-      }
-    } else {
-      for (int i = threadIdx.x; i < COUT * out_cells; i += G::THREADS) {
-        const int co = i / out_cells, j = i - co * out_cells;
-        out[(size_t)co * out_stride + j] = outs[co * OS + j];
+  if constexpr (W::NSTRIP > 1 && NH > 0) {
+    // strip boards: this strip's head sums over the cout tiles, in a fixed
+    // order, into the board-wide hfin [3][CS] (hp is reused by the next strip)
+    constexpr int SC = W::SCELLS;
+    for (int i = threadIdx.x; i < NH * SC; i += G::THREADS) {
+      const int hh = i / SC, lc = i - hh * SC;
+      if (c0 + lc < G::CELLS) {
+        float v = hp[hh * W::HS + lc];
+#pragma unroll
+        for (int mm = 1; mm < MT; ++mm) v += hp[(mm * 3 + hh) * W::HS + lc];
+        hfin[hh * G::CS + c0 + lc] = v;
       }
     }
   }
-  // no barrier: a caller that reads ``out`` back synchronises first
+  // whole-row stores (the tile-ordered epilogue would scatter 4-byte writes)
+  if (out != nullptr) {
+    if (out_stride == G::CS && out_cells == G::CS) {
+      const int Q = ((last ? G::CS : c0 + W::SCELLS) - c0) / 4;   // float4 of this strip's row span
+      for (int i = threadIdx.x; i < COUT * Q; i += G::THREADS) {
+        const int co = i / Q, q = i - co * Q;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(outs + co * OS + q * 4);
+        f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)co * G::CS + c0) + q;
+#if MZGO_NT_STORE
+        __builtin_nontemporal_store(v, dst);
+#else
+        *dst = v;
+#endif
+      }
+    } else {
+      const int n = min(c0 + W::SCELLS, out_cells) - c0;
+      for (int i = threadIdx.x; i < COUT * n; i += G::THREADS) {
+        const int co = i / n, j = i - co * n;
+        out[(size_t)co * out_stride + c0 + j] = outs[co * OS + j];
+      }
+    }
+  }
+  // no barrier: a caller that reads ``out`` (or hfin) back synchronises first
 }
 
 }  // namespace mzgo
