@@ -16,6 +16,7 @@ namespace mzgo {
 // 4 cell jobs per wave need every register).
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------
 // Board / latent geometry.  Cells are stored row-major (a = r*N + c, pass = N*N)
@@ -73,7 +74,9 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // scripts/microbench.py).  Thread 0 of each workgroup adds shader-clock
 // deltas per phase into mzgo_stamps[block][phase].
 // ---------------------------------------------------------------------------
-constexpr int kStampPhases = 32;   // 0-7 phases (thread 0), 8-19 per-wave conv loops, 20+ sub-phases
+// 0-7 phases (thread 0), 8-19 per-wave conv loops, 20-31 sub-phases,
+// 32-43 per-wave conv-input work, 44-55 per-wave conv-input barrier wait
+constexpr int kStampPhases = 56;
 #ifdef MZGO_STAMPS
 // Phase sums accumulate in LDS (a global read-modify-write per lap would put
 // an HBM round trip on the measured wave's critical path); flush() adds them

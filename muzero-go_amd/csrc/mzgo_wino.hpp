@@ -39,6 +39,12 @@
 #ifndef MZGO_WINO_PINB
 #define MZGO_WINO_PINB 1
 #endif
+#ifndef MZGO_WINO_PRIO
+#define MZGO_WINO_PRIO 1
+#endif
+#ifndef MZGO_WINO_PK
+#define MZGO_WINO_PK 1
+#endif
 #ifndef MZGO_WINO_XG
 #define MZGO_WINO_XG 2
 #endif
@@ -117,6 +123,35 @@ __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 5; ++b) d[a][b] = s[a * PW + b];
+  float* vb = V + (size_t)quad * 64 + t * 4 + e;         // quad index == (h*S4 + s4)*4 + kq
+  constexpr int XSTRIDE = 2 * S4 * 4 * 64;    // floats between xi planes
+#if MZGO_WINO_PK
+  // rows in pairs (0,1), (2,3) as packed f32x2 (v_pk_add/v_pk_fma: two rows
+  // per instruction); the factor-2 FMAs round exactly like mul + add
+  f32x2 u[2][5];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {               // BT2 along rows
+    u[0][b] = f32x2{d[0][b], d[1][b]} + f32x2{-d[2][b], d[2][b]};
+    u[1][b] = f32x2{d[2][b], d[3][b]} - f32x2{d[1][b], d[1][b]};
+  }
+  const f32x2 two = {2.f, 2.f}, mtwo = {-2.f, -2.f}, three = {3.f, 3.f};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {               // BT3 along columns
+    const f32x2* q = u[i];
+    const f32x2 a = q[1] - q[3], b = q[0] - q[2];
+    f32x2 v[5];
+    v[0] = __builtin_elementwise_fma(two, b, a);
+    v[1] = __builtin_elementwise_fma(three, q[2], __builtin_elementwise_fma(two, q[1], q[3]));
+    v[2] = __builtin_elementwise_fma(mtwo, q[1], q[2] + q[3]);
+    v[3] = a;
+    v[4] = __builtin_elementwise_fma(mtwo, a, q[4] - q[2]);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      vb[((2 * i) * 5 + j) * XSTRIDE] = v[j].x;
+      vb[((2 * i + 1) * 5 + j) * XSTRIDE] = v[j].y;
+    }
+  }
+#else
   float u[4][5];
 #pragma unroll
   for (int b = 0; b < 5; ++b) {               // BT2 along rows
@@ -125,8 +160,6 @@ __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const
     u[2][b] = d[2][b] - d[1][b];
     u[3][b] = d[3][b] - d[1][b];
   }
-  float* vb = V + (size_t)quad * 64 + t * 4 + e;         // quad index == (h*S4 + s4)*4 + kq
-  constexpr int XSTRIDE = 2 * S4 * 4 * 64;    // floats between xi planes
 #pragma unroll
   for (int i = 0; i < 4; ++i) {               // BT3 along columns
     const float* q = u[i];
@@ -136,6 +169,7 @@ __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const
     vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
     vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
   }
+#endif
 }
 
 // The halo columns of every raw plane must be 0 before the first wino_input
@@ -181,6 +215,7 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
   const float* ebase = emb ? emb : src;
 
   if (strip > 0) __syncthreads();            // the previous strip's epilogue is done with LDS
+  const unsigned long long t_in = st ? __builtin_amdgcn_s_memtime() : 0;
   if (fast) {
     // all of this wave's rows (and their embedding values) in flight at once;
     // loads are branch-free (clamped indices) so they stay outstanding together
@@ -220,8 +255,10 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
         for (int r = 0; r < 4; ++r) my[widx[p][r]] = rg[k][p][r] + ec;
       }
       wave_lds_sync();
+      if (st && k == 0) st->lap(29);
       wino_transform_quad<G, CIN>(V, my, quad, t, e, ty, tx);
     }
+    if (st) st->lap(30);
   } else {
     // strip rows row0 .. row0+PH-1 of the quad's 4 channels (rows off the
     // board are written as 0: the plane is reused by every strip)
@@ -258,8 +295,15 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
       wino_transform_quad<G, CIN>(V, my, quad, t, e, ty, tx);
     }
   }
+  unsigned long long t_pre = 0;
+  if (st) t_pre = __builtin_amdgcn_s_memtime();
   __syncthreads();
-  if (st) st->lap(21);
+  if (st) {
+    const unsigned long long t_post = __builtin_amdgcn_s_memtime();
+    st->wave_add(32 + wave, t_pre - t_in);
+    st->wave_add(44 + wave, t_post - t_pre);
+    st->lap(21);
+  }
 }
 
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
@@ -329,6 +373,15 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       if constexpr (2 * MT == G::WAVES)
         if (g > 0 && g % MZGO_WINO_SYNC == 0) __builtin_amdgcn_s_barrier();
 #endif
+#if MZGO_WINO_PRIO
+      // progress-ordered issue: a wave that is ahead drops its priority, so
+      // the SIMD's three waves advance together (oldest-first issue otherwise
+      // leaves the youngest wave's two MFMA chains to finish alone)
+      if (g == 0) __builtin_amdgcn_s_setprio(3);
+      else if (g == 1) __builtin_amdgcn_s_setprio(2);
+      else if (g == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+#endif
       f32x4 acc[XG];
 #pragma unroll
       for (int q = 0; q < XG; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -397,6 +450,9 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       else { yp[ox] = z0; yp[3 + ox] = z1 - z0; }
     }
   }
+#if MZGO_WINO_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   if (st) { st->wave_add(8 + wave, __builtin_amdgcn_s_memtime() - t_loop); st->lap(6); }
 
   // epilogue constants before any store (see conv3x3_ring)
