@@ -125,6 +125,9 @@ def main():
     ap.add_argument("--games", type=int, default=256, help="parallel games per GPU")
     ap.add_argument("--sims", type=int, default=200)
     ap.add_argument("--latent-dim", type=int, default=96)
+    ap.add_argument("--dynamics", choices=["factored", "direct"], default="factored",
+                    help="factored: one conv per parent, children as relu(Y + E[a]) (mzgo_expand.hpp); "
+                         "direct: a dynamics conv per simulation, as the reference computes it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
@@ -153,7 +156,7 @@ def main():
     if world > 1:
         from mzgo import distributed as mdist
         mdist.broadcast_weights(net)                      # one RCCL broadcast, untimed
-    sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G)
+    sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G, dynamics=args.dynamics)
     eng = sp.engine
     M = sp.max_moves
     stream = torch.cuda.current_stream()

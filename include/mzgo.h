@@ -64,6 +64,10 @@ typedef struct mzgo_config {
   uint64_t seed;            /* counter-RNG seed */
   int game_base;            /* global id of slot 0 (multi-GPU game sharding) */
   int device;               /* HIP device ordinal */
+  int direct_dynamics;      /* 0 = factored expansion (default): a search convolves each
+                               parent once and expands children as relu(Y + E[a]), exact
+                               up to fp32 rounding (see muzero-go_amd/csrc/mzgo_expand.hpp);
+                               1 = one dynamics conv per simulation, as the reference does */
 } mzgo_config;
 
 typedef struct mzgo_engine mzgo_engine;

@@ -140,6 +140,40 @@ std::vector<float> pack_wino(const float* W, int COUT, int CIN) {
   return out;
 }
 
+// The action-tap table of the factored expansion (mzgo_expand.hpp):
+// E[a][r][co] = sum over the taps (ky, kx) on the board for a cell of region
+// r = ry*3 + rx (ry, rx in {first, interior, last} row / column) of
+// sum_ci W[co][ci][ky][kx] * emb[a][ci], so that conv3x3(x + emb[a]) =
+// conv3x3(x) + E[a][region] under zero padding.  f64 sums, rounded once.
+std::vector<float> action_taps(const float* W, const float* emb, int C, int A) {
+  std::vector<float> out((size_t)A * 9 * C);
+  std::vector<double> u((size_t)9 * C);
+  for (int a = 0; a < A; ++a) {
+    const float* e = emb + (size_t)a * C;
+    for (int co = 0; co < C; ++co)
+      for (int t = 0; t < 9; ++t) {
+        double s = 0.0;
+        for (int ci = 0; ci < C; ++ci) s += (double)W[((size_t)co * C + ci) * 9 + t] * (double)e[ci];
+        u[(size_t)t * C + co] = s;
+      }
+    for (int r = 0; r < 9; ++r) {
+      const int ry = r / 3, rx = r % 3;
+      for (int co = 0; co < C; ++co) {
+        double s = 0.0;
+        for (int ky = 0; ky < 3; ++ky) {
+          if ((ry == 0 && ky == 0) || (ry == 2 && ky == 2)) continue;   // row y-1 / y+1 off the board
+          for (int kx = 0; kx < 3; ++kx) {
+            if ((rx == 0 && kx == 0) || (rx == 2 && kx == 2)) continue;
+            s += u[(size_t)(ky * 3 + kx) * C + co];
+          }
+        }
+        out[((size_t)a * 9 + r) * C + co] = (float)s;
+      }
+    }
+  }
+  return out;
+}
+
 }  // namespace
 
 struct mzgo_engine {
@@ -205,6 +239,7 @@ struct mzgo_engine {
                           "prediction.policy_conv.weight"})
       hw.insert(hw.end(), sd[k].begin(), sd[k].end());
     parts.push_back(hw);
+    parts.push_back(action_taps(sd["dynamics.conv.weight"].data(), sd["dynamics.action_embedding.weight"].data(), C, A));
     const char* scal[] = {"dynamics.reward_conv.bias", "dynamics.fc_reward_hidden.weight",
                           "dynamics.fc_reward_hidden.bias", "dynamics.fc_reward_output.weight",
                           "dynamics.fc_reward_output.bias", "prediction.value_conv.bias",
@@ -228,11 +263,11 @@ struct mzgo_engine {
     np.w_conv2 = b + off[2]; np.b_conv2 = b + off[3];
     np.w_conv3 = b + off[4]; np.b_conv3 = b + off[5];
     np.w_dyn = b + off[6]; np.b_dyn = b + off[7];
-    np.emb = b + off[8]; np.head_w = b + off[9];
-    np.hs.reward_b = b + off[10]; np.hs.fc1_w = b + off[11]; np.hs.fc1_b = b + off[12];
-    np.hs.fc2_w = b + off[13]; np.hs.fc2_b = b + off[14]; np.hs.value_b = b + off[15];
-    np.hs.vfc_w = b + off[16]; np.hs.vfc_b = b + off[17]; np.hs.policy_b = b + off[18];
-    np.hs.pass_logit = b + off[19];
+    np.emb = b + off[8]; np.head_w = b + off[9]; np.etab = b + off[10];
+    np.hs.reward_b = b + off[11]; np.hs.fc1_w = b + off[12]; np.hs.fc1_b = b + off[13];
+    np.hs.fc2_w = b + off[14]; np.hs.fc2_b = b + off[15]; np.hs.value_b = b + off[16];
+    np.hs.vfc_w = b + off[17]; np.hs.vfc_b = b + off[18]; np.hs.policy_b = b + off[19];
+    np.hs.pass_logit = b + off[20];
     dirty = false;
     return MZGO_OK;
   }
@@ -243,6 +278,7 @@ struct mzgo_engine {
     sp.dirichlet_alpha = cfg.dirichlet_alpha; sp.dirichlet_epsilon = cfg.dirichlet_epsilon;
     sp.pass_epsilon = cfg.pass_epsilon; sp.num_simulations = S; sp.compat = cfg.compat;
     sp.variant = cfg.search_variant;
+    sp.factored = cfg.direct_dynamics ? 0 : 1;
     sp.seed = cfg.seed;
     return sp;
   }
@@ -280,6 +316,8 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   if (cfg->num_games < 1) return fail(MZGO_EINVAL, "num_games must be >= 1");
   if (C != 0 && cfg->num_simulations < 1) return fail(MZGO_EINVAL, "num_simulations must be >= 1");
   if (cfg->compat != 0 && cfg->compat != 1) return fail(MZGO_EINVAL, "compat must be 0 or 1");
+  if (cfg->direct_dynamics != 0 && cfg->direct_dynamics != 1)
+    return fail(MZGO_EINVAL, "direct_dynamics must be 0 (factored expansion) or 1 (a conv per simulation)");
   if (cfg->search_variant != 0 && cfg->search_variant != 1)
     return fail(MZGO_EINVAL, "search_variant must be 0 (self_play.py) or 1 (main.py)");
   HIPCHK(hipSetDevice(cfg->device));
@@ -299,9 +337,10 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   int rc = MZGO_OK;
   auto chk = [&](int r) { if (r != MZGO_OK && rc == MZGO_OK) rc = r; };
   if (C != 0) {
-    chk(e->alloc(&E.pool, G * n1 * (size_t)C * e->CS));
+    // S+1 node slots + one scratch latent per game
+    chk(e->alloc(&E.pool, G * (n1 + 1) * (size_t)C * e->CS));
     // pad cells (>= N*N) of pooled latents are read as zeros and never written
-    if (rc == MZGO_OK && hipMemset(E.pool, 0, G * n1 * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
+    if (rc == MZGO_OK && hipMemset(E.pool, 0, G * (n1 + 1) * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
       chk(fail(MZGO_EHIP, "hipMemset(pool) failed"));
     chk(e->alloc(&E.prior, G * n1 * A));
     chk(e->alloc(&E.child, G * n1 * A));
@@ -310,6 +349,7 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     chk(e->alloc(&E.root_prior, G * A));
     chk(e->alloc(&E.path, G * (n1 + 1)));
     chk(e->alloc(&E.nodes, G));
+    chk(e->alloc(&E.nact, G * n1));
     chk(e->alloc(&E.rec_stones, G * M * CELLS));
     chk(e->alloc(&E.rec_invd, G * M * CELLS));
     chk(e->alloc(&E.rec_flags, G * M));

@@ -298,7 +298,7 @@ __device__ __forceinline__ typename WFrag<MGP>::T lds_frag(const float* p) {
 
 // hp_lds: head partials [2][3][CS]; written after a workgroup barrier, so it
 // may alias lds_in.  Returns with all waves synchronised.
-template <class G, int CIN, int COUT, int NH>
+template <class G, int CIN, int COUT, int NH, bool YM = false>
 __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, const float* __restrict__ wpk,
                                     const float* __restrict__ bias, float* __restrict__ out,
                                     int out_stride, int out_cells, const float* __restrict__ head_w,
@@ -493,10 +493,14 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
 #pragma unroll
           for (int ni = 0; ni < NG; ++ni) {
             float v = acc[j][mi][ni][r] + bb[mi][r];
-            v = v > 0.f ? v : 0.f;
+            if (!YM) v = v > 0.f ? v : 0.f;                 // YM: pre-activation conv + bias
             const int cell = ((cg0 + j * R::JPW) * NG + ni) * 16 + col;
             v = cell < G::CELLS ? v : 0.f;                  // pad cells stay 0 (zero slot)
-            if (out != nullptr && cell < out_cells) out[co * out_stride + cell] = v;
+            if constexpr (YM) {                             // cell-major [CELLS][COUT]
+              if (cell < G::CELLS) out[(size_t)cell * COUT + co] = v;
+            } else if (out != nullptr && cell < out_cells) {
+              out[co * out_stride + cell] = v;
+            }
 #pragma unroll
             for (int h = 0; h < NH; ++h) hsum[h][j][ni] = __builtin_fmaf(hw[h][mi][r], v, hsum[h][j][ni]);
           }

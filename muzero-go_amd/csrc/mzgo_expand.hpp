@@ -1,0 +1,159 @@
+// mzgo_expand.hpp -- the factored dynamics expansion.
+//
+// DynamicsNetwork.forward (self_play.py:85-95) computes, for a leaf latent x
+// and action a,   relu(conv3x3(x + emb[a] (broadcast over cells)) + b).
+// The convolution is linear and zero-padded, so
+//     conv3x3(x + emb[a]) + b  =  Y_x + E[a][region(cell)]
+// with Y_x = conv3x3(x) + b (one conv per distinct LEAF, not per child) and
+//     E[a][r][co] = sum over the taps (ky, kx) that stay on the board for a
+//                   cell of region r of  sum_ci W[co][ci][ky][kx] * emb[a][ci]
+// where r = (row class)*3 + (column class), classes {first, interior, last}.
+// E is a per-network table [A][9][C] built once on the host in f64
+// (mzgo_capi.hip: action_taps).
+//
+// A search therefore runs the full 3x3 conv only for nodes that become
+// parents (3-11 per 200-400-simulation search in the reference's trees; the
+// unexpanded-first rule, self_play.py:283-287, makes trees wide and shallow),
+// and every expansion is an elementwise pass over Y_leaf:
+//     child latent = relu(Y_leaf + E[a])            (never stored: rebuilt by
+//                                                    materialize() if the child
+//                                                    ever becomes a parent)
+//     reward/value/policy 1x1 heads over it         (self_play.py:91-94, :105-112)
+// Every output of recurrent_inference is still computed for every
+// simulation; only the conv of a leaf is shared by its children.  The fp32
+// sums differ from torch's by rounding only (emb is added after the conv
+// rather than before), like the Winograd conv.
+//
+// Y is stored cell-major, [CELLS][C] per node, so 8 lanes read one cell's
+// channels as contiguous float4s.
+#pragma once
+#include "mzgo_common.hpp"
+
+namespace mzgo {
+
+template <class G>
+struct ExpandShape {
+  static constexpr int C4 = G::C / 4;         // float4 per cell
+  static constexpr int LPC = 8;               // lanes per cell
+  static constexpr int PERL = C4 / LPC;       // float4 per lane
+  static constexpr int CPP = G::THREADS / LPC;   // cells per pass
+  static constexpr int PASSES = (G::CELLS + CPP - 1) / CPP;
+  static_assert(G::C % 32 == 0, "8 lanes x whole float4s per cell");
+};
+
+// LDS of the expansion: the heads, and (if they fit beside the conv buffers
+// they share a union with) a copy of one node's Y and of the 1x1 head
+// weights, so that consecutive expansions of the same leaf read them from LDS
+// instead of L2.  A conv (rare) overwrites the union; the next expansion
+// refills it.
+template <class G, bool FITS>
+struct ExpandLds {
+  static constexpr bool CACHE = FITS;
+  alignas(16) float yc[FITS ? G::CELLS * G::C : 4];
+  alignas(16) float hw[FITS ? 3 * G::C : 4];
+  float xh[3 * G::CS];
+};
+
+// board region class of a cell: (row class) * 3 + (column class)
+template <class G>
+__device__ __forceinline__ int region_of(int cell) {
+  const int y = cell / G::N, x = cell - y * G::N;
+  const int ry = y == 0 ? 0 : (y == G::N - 1 ? 2 : 1);
+  const int rx = x == 0 ? 0 : (x == G::N - 1 ? 2 : 1);
+  return ry * 3 + rx;
+}
+
+// 8-lane sum (lanes 8k .. 8k+7) via DPP: quad xor 1, xor 2, then half-row mirror
+__device__ __forceinline__ float sum8(float v) {
+  v = v + dpp::mov<dpp::XOR1>(v);
+  v = v + dpp::mov<dpp::XOR2>(v);
+  return v + dpp::mov<0x141>(v);              // row_half_mirror: lane i <-> 7 - i
+}
+
+// Child heads of expansion (leaf, a): L.xh [3][CS] gets, per cell, the
+// reward, value and policy 1x1-conv sums (no biases) of relu(Y + E[a]).
+// Y: the leaf's [CELLS][C] (global; read from the LDS copy L.yc when
+// ``hit``, else copied into it); ea: E[a] [9][C]; hw [3][C] (global: reward,
+// value, policy conv weights; L.hw is their LDS copy, valid with L.yc).  All
+// threads; the caller synchronises before reading xh.
+template <class G, class L>
+__device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y, bool hit,
+                                             const float* __restrict__ ea, const float* hw) {
+  typedef ExpandShape<G> X;
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(Y);
+  const f32x4* E4 = reinterpret_cast<const f32x4*>(ea);
+  const bool lw = L::CACHE && hit;
+  const f32x4* W4 = reinterpret_cast<const f32x4*>(hw);
+  f32x4* C4 = reinterpret_cast<f32x4*>(lds.yc);
+  f32x4* CW = reinterpret_cast<f32x4*>(lds.hw);
+  const int j = threadIdx.x & (X::LPC - 1);
+#pragma unroll
+  for (int pass = 0; pass < X::PASSES; ++pass) {
+    const int cell = pass * X::CPP + threadIdx.x / X::LPC;
+    const int cl = cell < G::CELLS ? cell : G::CELLS - 1;
+    const int reg = region_of<G>(cl);
+    f32x4 y[X::PERL], e[X::PERL];
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) e[k] = E4[reg * X::C4 + j + X::LPC * k];
+    if (L::CACHE && hit) {
+#pragma unroll
+      for (int k = 0; k < X::PERL; ++k) y[k] = C4[(size_t)cl * X::C4 + j + X::LPC * k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < X::PERL; ++k) y[k] = Y4[(size_t)cl * X::C4 + j + X::LPC * k];
+      if (L::CACHE && cell < G::CELLS) {
+#pragma unroll
+        for (int k = 0; k < X::PERL; ++k) C4[(size_t)cl * X::C4 + j + X::LPC * k] = y[k];
+      }
+    }
+    float hr = 0.f, hv = 0.f, hp = 0.f;
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) {
+      const int c4 = j + X::LPC * k;
+      f32x4 wr, wv, wp;
+      if (lw) {
+        wr = CW[c4]; wv = CW[X::C4 + c4]; wp = CW[2 * X::C4 + c4];
+      } else {
+        wr = W4[c4]; wv = W4[X::C4 + c4]; wp = W4[2 * X::C4 + c4];
+        if (L::CACHE && pass == 0 && threadIdx.x < X::LPC) {   // one writer per weight
+          CW[c4] = wr; CW[X::C4 + c4] = wv; CW[2 * X::C4 + c4] = wp;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = y[k][q] + e[k][q];
+        v = v > 0.f ? v : 0.f;
+        hr = __builtin_fmaf(wr[q], v, hr);
+        hv = __builtin_fmaf(wv[q], v, hv);
+        hp = __builtin_fmaf(wp[q], v, hp);
+      }
+    }
+    hr = sum8(hr);
+    hv = sum8(hv);
+    hp = sum8(hp);
+    if (j == 0 && cell < G::CELLS) {
+      lds.xh[cell] = hr;
+      lds.xh[G::CS + cell] = hv;
+      lds.xh[2 * G::CS + cell] = hp;
+    }
+  }
+}
+
+// The latent of a node that is about to become a parent: relu(Y_par + E[a])
+// -> dst [C][CS] (channel-major, pad cells 0), the layout the 3x3 conv reads.
+// All threads; the caller synchronises before the conv reads dst.
+template <class G>
+__device__ __forceinline__ void materialize(float* __restrict__ dst, const float* __restrict__ Ypar,
+                                            const float* __restrict__ ea) {
+  for (int i = threadIdx.x; i < G::C * G::CS; i += G::THREADS) {
+    const int c = i / G::CS, p = i - c * G::CS;
+    float v = 0.f;
+    if (p < G::CELLS) {
+      v = Ypar[(size_t)p * G::C + c] + ea[region_of<G>(p) * G::C + c];
+      v = v > 0.f ? v : 0.f;
+    }
+    dst[i] = v;
+  }
+}
+
+}  // namespace mzgo

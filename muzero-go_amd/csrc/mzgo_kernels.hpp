@@ -6,6 +6,7 @@
 #pragma once
 #include "mzgo_board.hpp"
 #include "mzgo_conv.hpp"
+#include "mzgo_expand.hpp"
 #include "mzgo_search.hpp"
 #include "mzgo_wino.hpp"
 
@@ -19,6 +20,7 @@ struct NetParams {
   const float* w_dyn;   const float* b_dyn;     // dynamics.conv (C -> C)
   const float* emb;                             // dynamics.action_embedding [A][C]
   const float* head_w;                          // [3][C]: reward_conv, value_conv, policy_conv
+  const float* etab;                            // [A][9][C] action-tap table (mzgo_expand.hpp)
   HeadScalars hs;
 };
 
@@ -27,7 +29,8 @@ struct EngineArrays {
   int S;                 // simulations per move this engine was sized for
   int max_moves;
   // search state
-  float* pool;           // [G][S+1][C][CS] latents, node-indexed
+  float* pool;           // [G][S+2][C*CS] per node: latent [C][CS] (direct dynamics) or conv
+                         // output Y [CELLS][C] (factored); slot S+1: scratch latent
   float* prior;          // [G][S+1][A]
   int* child;            // [G][S+1][A]
   int* visits;           // [G][S+1]
@@ -35,6 +38,7 @@ struct EngineArrays {
   double* root_prior;    // [G][A]
   int* path;             // [G][S+2]
   int* nodes;            // [G]  nodes used by the last search
+  int* nact;             // [G][S+1] action that created each node (factored: rebuilds its latent)
   // boards
   int8_t* stones;        // [G][CELLS]
   uint8_t* invd;         // [G][CELLS]
@@ -76,6 +80,7 @@ struct Smem {
     float in[G::CINMAX * G::CPAD];                       // conv staging
     float hp[2 * 3 * G::CS];                             // head partials (after the conv loop)
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
+    ExpandLds<G, G::CELLS * G::C + 3 * G::CS + 3 * G::C <= G::CINMAX * G::CPAD> f;   // factored expansion
   } u;
   alignas(16) float ring[RingBytes<G>::value / 4];       // weight DMA ring
   TreeLds<G> t;
@@ -100,6 +105,7 @@ struct Smem<G, true> {
       alignas(16) float outs[G::C * Wino<G>::OUT_STRIDE];   // conv output staging
     } x;
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
+    ExpandLds<G, G::CELLS * G::C + 3 * G::CS + 3 * G::C <= Wino<G>::template v_floats<G::CINMAX>()> f;
   } u;
   alignas(16) float raw[WinoRaw<G>::FLOATS];              // per-wave staging of conv input rows
   static constexpr bool STRIPS = Wino<G>::NSTRIP > 1;
@@ -117,7 +123,7 @@ struct Smem<G, true> {
 // One latent conv: src ([CIN][src_stride], global) (+ emb per channel) ->
 // dst ([COUT][dst_stride], cells < out_cells), NH fused 1x1 head partials left
 // in sm.heads().  All threads; returns synchronised.
-template <class G, int CIN, int COUT, int NH>
+template <class G, int CIN, int COUT, int NH, bool YM = false>
 __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict__ w, const float* __restrict__ b,
                                             const float* src, int src_stride, const float* emb, float* dst,
                                             int dst_stride, int out_cells, const float* head_w,
@@ -128,7 +134,7 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
     for (int s = 0; s < Wino<G>::NSTRIP; ++s) {
       wino_input<G, CIN>(sm.u.v, sm.raw, src, src_stride, emb, s, st);
       if (st) st->lap(1);
-      wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, w, b, dst, dst_stride,
+      wino_conv<G, CIN, COUT, NH, YM>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, w, b, dst, dst_stride,
                                   out_cells, head_w, s, st);
     }
     if constexpr (Wino<G>::NSTRIP > 1) __syncthreads();   // hfin complete
@@ -136,7 +142,7 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
     stage_board<G>(sm.u.in, src, src_stride, CIN, emb);
     __syncthreads();
     if (st) st->lap(1);
-    conv3x3_ring<G, CIN, COUT, NH>(sm.u.in, sm.ring, w, b, dst, dst_stride, out_cells, head_w, sm.u.hp, st);
+    conv3x3_ring<G, CIN, COUT, NH, YM>(sm.u.in, sm.ring, w, b, dst, dst_stride, out_cells, head_w, sm.u.hp, st);
   }
 }
 
@@ -242,18 +248,29 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 // ---------------------------------------------------------------------------
 // One full MCTS.run (self_play.py:148-237) for game slot g.
 // ---------------------------------------------------------------------------
+// Game g's node slots: S+1 nodes + one scratch latent (slot S+1).
+template <class G>
+__device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
+  return E.pool + (size_t)g * ((size_t)E.S + 2) * G::C * G::CS;
+}
+
 // The simulations of one search with the tree accessor Acc (LDS or HBM stats).
 template <class G, class Acc>
 __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                          const EngineArrays& E, int g, const TreeView& TV, uint64_t key) {
-  float* pool = E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS;
+  float* pool = pool_of<G>(E, g);
   const size_t node_floats = (size_t)G::C * G::CS;
+  float* scratch = pool + (size_t)(E.S + 1) * node_floats;
+  int* nact = E.nact + (size_t)g * ((size_t)E.S + 1);
   const int S = sp.num_simulations;
+  const bool factored = sp.factored != 0;
   Acc T(TV, sm.t);
   tree_reset_root<G>(T);
   if (threadIdx.x == 0) { sm.t.newest = -1; sm.t.newp_node = -1; }
   __syncthreads();
 
+  if (threadIdx.x == 0) sm.t.ycache = -1;               // the union holds no node's Y yet
+  __syncthreads();
   int nodes = 1;
   Stamp st(E.stamps);
   for (int sim = 0; sim < S; ++sim) {
@@ -272,24 +289,51 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     }
     const int nid = nodes++;
     if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
-    latent_conv<G, G::C, G::C, 3>(sm, np.w_dyn, np.b_dyn, pool + (size_t)leaf * node_floats, G::CS,
-                                  np.emb + (size_t)a * G::C, pool + (size_t)nid * node_floats, G::CS, G::CS,
-                                  np.head_w, &st);
+    const float* heads;
+    if (factored) {
+      // the leaf's conv Y exists once it has a child; otherwise compute it now
+      // (from its latent, rebuilt from its parent's Y unless it is the root)
+      float* yleaf = pool + (size_t)leaf * node_floats;
+      int yc = sm.t.ycache;
+      if (!sm.t.yready) {
+        if (leaf != 0) {
+          const int par = T.path(depth - 1);
+          materialize<G>(scratch, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C);
+          __syncthreads();
+        }
+        latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS, G::CS,
+                                            nullptr, &st);
+        __syncthreads();                                 // Y stores before the expansion reads them
+        yc = -1;                                         // the conv overwrote the LDS copy
+      }
+      expand_heads<G>(sm.u.f, yleaf, yc == leaf, np.etab + (size_t)a * 9 * G::C, np.head_w);
+      __syncthreads();
+      if (threadIdx.x == 0 && decltype(sm.u.f)::CACHE) sm.t.ycache = leaf;   // read by all before the barrier
+      heads = sm.u.f.xh;
+    } else {
+      latent_conv<G, G::C, G::C, 3>(sm, np.w_dyn, np.b_dyn, pool + (size_t)leaf * node_floats, G::CS,
+                                    np.emb + (size_t)a * G::C, pool + (size_t)nid * node_floats, G::CS, G::CS,
+                                    np.head_w, &st);
+      heads = sm.heads();
+    }
     st.lap(2);
     // wave 1: policy logits -> the new node's priors (published in LDS for a
     // select that reaches it); wave 0, meanwhile: value/reward heads, backup
     // and (next iteration) the next select.  Wave 0 issues no HBM stores, so
     // its tree loads never wait for store acks.  The select barrier joins them.
     if (wave_id() == 1) {
-      heads_logits<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, sm.t.logits);
+      int* crow = TV.child + (size_t)nid * G::A;        // the new node: no children yet
+      for (int i = lane_id(); i < G::A; i += 64) crow[i] = -1;   // (before its priors are published)
+      if (factored) heads_logits<G, 1>(heads, true, sm.t.hsc, sm.t.logits);
+      else heads_logits<G, Smem<G>::HEAD_PARTS>(heads, true, sm.t.hsc, sm.t.logits);
       child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A, nid, sp.variant);
-      int* crow = TV.child + (size_t)nid * G::A;      // the new node: no children yet
-      for (int i = lane_id(); i < G::A; i += 64) crow[i] = -1;
     }
     if (wave_id() == 0) {
       float r, v;
-      heads_value<G, Smem<G>::HEAD_PARTS>(sm.heads(), true, sm.t.hsc, r, v);
+      if (factored) heads_value<G, 1>(heads, true, sm.t.hsc, r, v);
+      else heads_value<G, Smem<G>::HEAD_PARTS>(heads, true, sm.t.hsc, r, v);
       if (lane_id() == (a & 63)) T.set_child(leaf, a, nid);
+      if (lane_id() == 0) nact[nid] = a;
       backup<G>(T, depth, nid, (double)r + sp.discount * (double)v, sp.variant == 0);
     }
     st.lap(3);
@@ -307,9 +351,14 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
                                   uint64_t key) {
   const TreeView TV = TreeViewOf<G>::make(E, g);
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
-  float* root = E.pool + (size_t)g * ((size_t)E.S + 1) * G::C * G::CS;
-  representation<G>(sm, np, planes, root, G::CS,
-                    root + (size_t)G::C * G::CS);        // root latent -> node 0 (node 1's slot: scratch)
+  float* pool = pool_of<G>(E, g);
+  const size_t node_floats = (size_t)G::C * G::CS;
+  // root latent: node 0's slot (direct; node 1's slot is strip-conv scratch) or
+  // the scratch slot (factored: node 0's slot receives its conv Y)
+  if (sp.factored)
+    representation<G>(sm, np, planes, pool + (size_t)(E.S + 1) * node_floats, G::CS, pool);
+  else
+    representation<G>(sm, np, planes, pool, G::CS, pool + node_floats);
   if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
   __syncthreads();
   if constexpr (G::TREE_CAP > 0) {

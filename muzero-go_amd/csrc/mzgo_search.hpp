@@ -25,6 +25,7 @@ struct SearchParams {
   int num_simulations;      // S
   int compat;               // 0: reference (zero visit counts), 1: fixed
   int variant;              // 0: self_play.py MCTS, 1: main.py MCTS (main.py:246-368)
+  int factored;             // 1: factored dynamics expansion (mzgo_expand.hpp), 0: a conv per simulation
   uint64_t seed;
 };
 
@@ -49,6 +50,8 @@ struct TreeLds {
   double pass_prior;       // 0.01 or 1.0
   float reward, value;
   int leaf, action, nid, depth, nodes, bcast;
+  int yready;              // select's leaf already has a child (its conv Y exists: factored mode)
+  int ycache;              // node whose Y the LDS copy holds (factored mode), -1: none
   float hsc[64];                   // staged HeadScalars (HS_* offsets)
   // LDS-resident tree state (boards with G::TREE_CAP > 0 and S + 2 <= TREE_CAP)
   int svis[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
@@ -403,7 +406,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         __builtin_amdgcn_s_sleep(1);
     double P[G::AP];
     int ch[G::AP];
-    uint64_t anypos = 0, elig[G::AP], unexp[G::AP];
+    uint64_t anypos = 0, anych = 0, elig[G::AP], unexp[G::AP];
     int n_unexp = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
@@ -422,6 +425,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       const bool pos = in && P[j] > 0.0;
       const bool e = pos && mask_of<G>(t, a) > 0.0;
       anypos |= __ballot(pos);
+      anych |= __ballot(in && ch[j] >= 0);
       elig[j] = __ballot(e);
       unexp[j] = __ballot(e && ch[j] < 0);
       n_unexp += __popcll(unexp[j]);
@@ -455,6 +459,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       }
       t.leaf = node;
       t.depth = depth;
+      t.yready = anych != 0 ? 1 : 0;
       return best;
     }
 

@@ -325,7 +325,7 @@ __device__ __forceinline__ constexpr float wino_at3(int ox, int j) {
 // xi = h*10 + xl and k-position k (pack_wino).  out: [COUT][out_stride]
 // global; cells >= out_cells are not stored (pooled rows, stride == out_cells
 // == CS, are stored whole with their zero pad cells).
-template <class G, int CIN, int COUT, int NH>
+template <class G, int CIN, int COUT, int NH, bool YM = false>
 __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, float* outs, float* hfin,
                                           const float* __restrict__ upk,
                                           const float* __restrict__ bias, float* __restrict__ out,
@@ -506,7 +506,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         const float mine = ymine[ox][r];
         // fixed order: (xi half 0) + (xi half 1)
         float v = (h == 0 ? mine + other : other + mine) + bb[r];
-        v = v > 0.f ? v : 0.f;
+        if (!YM) v = v > 0.f ? v : 0.f;           // YM: pre-activation conv + bias
         v = valid ? v : 0.f;
         const int co = m * 16 + kq * 4 + r;
         outs[co * OS + (valid ? cell - c0 : W::OCELLS)] = v;   // staged (off-board lanes: junk cell)
@@ -550,7 +550,18 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     }
   }
   // whole-row stores (the tile-ordered epilogue would scatter 4-byte writes)
-  if (out != nullptr) {
+  if constexpr (YM) {
+    // cell-major [CELLS][COUT] (the factored expansion reads a cell's channels
+    // as contiguous float4s): float4 of 4 couts per (cell, cout quad)
+    constexpr int Q = COUT / 4;
+    const int n = min(c0 + W::SCELLS, G::CELLS) - c0;
+    for (int i = threadIdx.x; i < n * Q; i += G::THREADS) {
+      const int j = i / Q, q = i - j * Q;
+      const f32x4 v = {outs[(4 * q) * OS + j], outs[(4 * q + 1) * OS + j], outs[(4 * q + 2) * OS + j],
+                       outs[(4 * q + 3) * OS + j]};
+      reinterpret_cast<f32x4*>(out + (size_t)(c0 + j) * COUT)[q] = v;
+    }
+  } else if (out != nullptr) {
     if (out_stride == G::CS && out_cells == G::CS) {
       const int Q = ((last ? G::CS : c0 + W::SCELLS) - c0) / 4;   // float4 of this strip's row span
       for (int i = threadIdx.x; i < COUT * Q; i += G::THREADS) {

@@ -39,6 +39,7 @@ class Config(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("game_base", ctypes.c_int),
         ("device", ctypes.c_int),
+        ("direct_dynamics", ctypes.c_int),
     ]
 
 

@@ -36,6 +36,7 @@ class EngineConfig:
     seed: int = 1234
     game_base: int = 0
     device: int = 0
+    dynamics: str = "factored"    # "factored" (conv once per parent, mzgo_expand.hpp) or "direct"
 
     def to_c(self):
         c = _lib.Config()
@@ -50,6 +51,11 @@ class EngineConfig:
                 if v not in ("self_play", "main"):
                     raise ValueError(f"search_variant must be 'self_play' or 'main', not {v!r}")
                 v = 0 if v == "self_play" else 1
+            if f.name == "dynamics":
+                if v not in ("factored", "direct"):
+                    raise ValueError(f"dynamics must be 'factored' or 'direct', not {v!r}")
+                c.direct_dynamics = 0 if v == "factored" else 1
+                continue
             setattr(c, f.name, v)
         return c
 

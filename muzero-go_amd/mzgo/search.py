@@ -62,7 +62,7 @@ class TreeNode:
 class MCTS:
     def __init__(self, muzero_net, action_size, num_simulations, c_puct=2.5, *, compat="reference",
                  seed=1234, game=0, dirichlet_alpha=0.15, dirichlet_epsilon=0.02, discount=0.99,
-                 pass_epsilon=0.01):
+                 pass_epsilon=0.01, dynamics="factored"):
         if not isinstance(muzero_net, MuZeroNet):
             raise TypeError("mzgo.MCTS searches with an mzgo.MuZeroNet (HIP engine); got "
                             f"{type(muzero_net).__name__}")
@@ -74,7 +74,7 @@ class MCTS:
         self.c_puct = c_puct
         self.cfg = dict(c_puct=c_puct, compat=compat, seed=seed, game_base=game,
                         dirichlet_alpha=dirichlet_alpha, dirichlet_epsilon=dirichlet_epsilon,
-                        discount=discount, pass_epsilon=pass_epsilon)
+                        discount=discount, pass_epsilon=pass_epsilon, dynamics=dynamics)
         self.compat = compat
         self.root_child_visits = None
 

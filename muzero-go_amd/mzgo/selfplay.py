@@ -99,7 +99,7 @@ class SelfPlay:
     def __init__(self, net, num_games, num_simulations, *, seed=1234, compat="reference",
                  max_moves=0, temperature=1.0, temperature_moves=15, komi=0.0, game_base=0,
                  discount=0.99, c_puct=2.5, dirichlet_alpha=0.15, dirichlet_epsilon=0.02,
-                 pass_epsilon=0.01, search_variant="self_play"):
+                 pass_epsilon=0.01, search_variant="self_play", dynamics="factored"):
         self.net = net
         self.N = net.board_size
         self.G = num_games
@@ -111,7 +111,7 @@ class SelfPlay:
                                  game_base=game_base, discount=discount, c_puct=c_puct,
                                  dirichlet_alpha=dirichlet_alpha,
                                  dirichlet_epsilon=dirichlet_epsilon, pass_epsilon=pass_epsilon,
-                                 search_variant=search_variant)
+                                 search_variant=search_variant, dynamics=dynamics)
         self.max_moves = self.engine.M
         self.epoch = 0
 

@@ -29,8 +29,9 @@ def _net(N, C=96):
     return net
 
 
+@pytest.mark.parametrize("dynamics", ["factored", "direct"])
 @pytest.mark.parametrize("case", CASES)
-def test_search_matches_reference_tree(golden_dir, case):
+def test_search_matches_reference_tree(golden_dir, case, dynamics):
     import mzgo
     from oracle.mcts import tree_summary
     from oracle.rng import injected_noise
@@ -39,7 +40,7 @@ def test_search_matches_reference_tree(golden_dir, case):
     seed, game, move = int(g["seed"]), int(g["game"]), int(g["move"])
     A = N * N + 1
     net = _net(N)
-    mcts = mzgo.MCTS(net, A, S, seed=seed, game=game)
+    mcts = mzgo.MCTS(net, A, S, seed=seed, game=game, dynamics=dynamics)
     noise = torch.from_numpy(injected_noise(seed, game, move, A))
     root, visit_counts, root_value = mcts.run(g["obs"], move_index=move, noise=noise)
     assert not visit_counts.any()                       # reference bug reproduced (compat)
@@ -68,6 +69,31 @@ def test_batched_search_equals_single_searches():
         v1, val1 = e1.search(torch.from_numpy(obs[i:i + 1]), move_index=3)
         np.testing.assert_array_equal(v1.cpu().numpy()[0], vis_b[i])
         assert val1.item() == val_b[i]
+
+
+@pytest.mark.parametrize("N,S,moves", [(5, 40, 6), (6, 128, 10), (9, 200, 20), (19, 300, 60)])
+def test_factored_expansion_equals_direct_conv(N, S, moves):
+    """The factored expansion (conv once per parent, children as relu(Y +
+    E[a]); mzgo_expand.hpp) against a dynamics conv per simulation, the
+    reference's formulation (self_play.py:85-95), on G mid-game roots: the same
+    trees (node for node), child priors and root values up to fp32 rounding."""
+    from oracle.positions import random_position
+    G = 8
+    net = _net(N)
+    obs = torch.from_numpy(np.stack([random_position(N, moves + i, 300 + i) for i in range(G)]))
+    out = {}
+    for dyn in ("factored", "direct"):
+        eng = net.engine(num_games=G, num_simulations=S, seed=11, dynamics=dyn)
+        vis, val = eng.search(obs, move_index=moves)
+        out[dyn] = (vis.cpu().numpy(), val.cpu().numpy(), [eng.tree(g) for g in range(G)])
+    (vf, rf, tf), (vd, rd, td) = out["factored"], out["direct"]
+    np.testing.assert_array_equal(vf, vd)
+    np.testing.assert_allclose(rf, rd, rtol=0, atol=1e-5)
+    for a, b in zip(tf, td):
+        np.testing.assert_array_equal(a["child"], b["child"])
+        np.testing.assert_array_equal(a["visits"], b["visits"])
+        np.testing.assert_allclose(a["prior"][1:], b["prior"][1:], rtol=1e-4, atol=1e-7)
+        np.testing.assert_allclose(a["value_sum"], b["value_sum"], rtol=0, atol=1e-4)
 
 
 def test_sampled_dirichlet_statistics():
