@@ -42,23 +42,22 @@ def algorithmic_flops(N, C, S):
     return sim, root
 
 
-def executed_mfma_flops(N, C, S):
-    """MFMA FLOPs the kernel actually issues per move (16x16x4 f32: 2048 each).
+def algorithmic_bytes(N, C, G):
+    """SURVEY.md §8(d)'s algorithmic bytes per simulation (fp32): parent latent
+    read + child latent write 2*C*N^2*4, tree traffic at depth d = 2 (A child
+    priors / ids / visits / value sums, 20 B each, + 12 B backup per level),
+    the new node's priors A*4, and the weights amortised over G games."""
+    A = N * N + 1
+    return 2 * C * N * N * 4 + 2 * A * 20 + 2 * 12 + A * 4 + (9 * C * C + 3 * C + A * C) * 4 // G
 
-    9x9 runs its latent convs as Winograd F(2,3)xF(3,3) GEMMs (mzgo_wino.hpp):
-    20 transform points x (COUT/16) cout tiles x (CIN/4) k-steps, one 16-column
-    tile of 15 board tiles.  Other boards: the direct implicit GEMM over
-    16-cell column tiles.  conv1 (6 -> 64, cin padded to 8) is always direct.
-    """
-    ct = (N * N + 15) // 16
-    conv1 = 9 * 2 * (64 // 16) * ct
+
+def mfma_per_conv(N, cin, cout):
+    """16x16x4 f32 MFMAs of one 3x3 conv of one board (Winograd at 9x9 / 19x19)."""
     if N == 9:
-        wino = lambda cin, cout: 20 * (cout // 16) * (cin // 4)
-        dyn, rep = wino(C, C), wino(64, 64) + wino(64, C)
-    else:
-        direct = lambda cin, cout: 9 * (cin // 4) * (cout // 16) * ct
-        dyn, rep = direct(C, C), direct(64, 64) + direct(64, C)
-    return 2048 * (S * dyn + conv1 + rep)
+        return 20 * (cout // 16) * (cin // 4)
+    if N == 19:
+        return 5 * 20 * (cout // 16) * (cin // 4)
+    return 9 * (cin // 4) * (cout // 16) * ((N * N + 15) // 16)
 
 
 def cpu_baseline(N, C, S, budget_s=12.0):
@@ -213,10 +212,43 @@ def main():
     if rank == 0:
         sim_f, root_f = algorithmic_flops(N, C, S)
         per_launch_moves = moves / world / args.steps
+        per_launch_sims = sims / world / args.steps
         launch_flops = per_launch_moves * (S * sim_f + root_f)
-        achieved = launch_flops / avg_kern_s / 1e12
-        mfma_exec = per_launch_moves * executed_mfma_flops(N, C, S) / avg_kern_s / 1e12
-        peak = 157.3
+        equiv_tflops = launch_flops / avg_kern_s / 1e12      # the reference formulation's FLOP rate
+        convs = c1["dynamics_convs"] - c0["dynamics_convs"]
+        ct = (N * N + 15) // 16
+        # executed MFMA work: the dynamics convs the searches ran + the
+        # representation (conv1 direct, conv2/conv3 latent convs) per move
+        mfma_launch = 2048 * (convs / args.steps * mfma_per_conv(N, C, C) + per_launch_moves * (
+            9 * 2 * 4 * ct + mfma_per_conv(N, 64, 64) + mfma_per_conv(N, 64, C)))
+        mfma_exec = mfma_launch / avg_kern_s / 1e12
+        peak_mfma = 157.3
+        bytes_sim = algorithmic_bytes(N, C, G)
+        gbps = per_launch_sims * bytes_sim / avg_kern_s / 1e9
+        peak_hbm = 8000.0
+        if args.dynamics == "factored":
+            # one 3x3 conv per new PARENT (a few per search) instead of one per
+            # simulation: the MFMA roofline of the reference formulation no longer
+            # binds (equiv_direct_conv_tflops exceeds the fp32 MFMA peak); the
+            # remaining per-simulation work is latency-bound tree + elementwise
+            # traffic, reported against HBM with §8(d)'s bytes per simulation
+            roof = {"bound": "hbm", "kernel": "k_selfplay_move", "achieved": gbps, "peak": peak_hbm,
+                    "unit": "GB/s", "frac": gbps / peak_hbm, "traffic": None,
+                    "algorithmic_bytes_per_sim": bytes_sim, "sims_per_launch": per_launch_sims,
+                    "avg_launch_ms": avg_kern_s * 1e3,
+                    "equiv_direct_conv_tflops": equiv_tflops,
+                    "equiv_direct_conv_frac_of_fp32_mfma": equiv_tflops / peak_mfma,
+                    "dynamics_convs_per_move": convs / max(1.0, moves / world),
+                    "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak_mfma,
+                    "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a]))"}
+        else:
+            roof = {"bound": "mfma", "kernel": "k_selfplay_move", "achieved": equiv_tflops,
+                    "peak": peak_mfma, "unit": "TFLOP/s", "frac": equiv_tflops / peak_mfma, "traffic": None,
+                    "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3,
+                    # what the MFMA pipes actually execute (Winograd issues fewer
+                    # MFMA FLOPs than the direct conv's algorithmic count)
+                    "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak_mfma,
+                    "algorithm": "winograd F(2,3)xF(3,3)" if N in (9, 19) else "direct implicit GEMM"}
         out = {
             "metric": "MCTS simulations/sec (whole node) + self-play moves/sec, 9x9 Go, 200 sims/move",
             "value": sims / dt,
@@ -233,19 +265,15 @@ def main():
             "moves_per_s": moves / dt,
             "config": {"workload": f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move",
                        "board_size": N, "latent_dim": C, "games_per_gpu": G, "sims_per_move": S,
-                       "parallelism": f"game-sharded x{world}", "compat": "reference"},
-            "roofline": {"bound": "mfma", "kernel": "k_selfplay_move", "achieved": achieved,
-                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                         "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3,
-                         # what the MFMA pipes actually execute (Winograd on 9x9 issues
-                         # fewer MFMA FLOPs than the direct conv's algorithmic count)
-                         "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak,
-                         "algorithm": "winograd F(2,3)xF(3,3)" if N == 9 else "direct implicit GEMM"},
+                       "parallelism": f"game-sharded x{world}", "compat": "reference",
+                       "dynamics": args.dynamics},
+            "roofline": roof,
         }
         prof = os.path.join(ROOT, "profiles", "latest_summary.json")
         if os.path.exists(prof):
             p = json.load(open(prof))
-            if p.get("workload") == out["config"]["workload"] and "k_selfplay_move" in p.get("kernel", ""):
+            if (p.get("workload") == out["config"]["workload"] and "k_selfplay_move" in p.get("kernel", "")
+                    and p.get("dynamics", "direct") == args.dynamics):
                 # HBM bytes per launch from rocprofv3 PMC passes of this same command
                 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/summarize_profile.py)
                 out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]

@@ -130,9 +130,10 @@ int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uin
 
 /* Self-play.  selfplay_reset starts a new game in every slot (epoch = RNG
  * generation of the games); selfplay_move plays one move in every unfinished
- * slot.  selfplay_counters (host, synchronises; cumulative over the engine's
- * life): [0] simulations run, [1] moves played, [2] games finished, and
- * [3] slots still playing now. */
+ * slot.  selfplay_counters (host u64 [5], synchronises; cumulative over the
+ * engine's life): [0] simulations run, [1] moves played, [2] games finished,
+ * [3] slots still playing now, [4] dynamics 3x3 convs run by searches (one per
+ * expansion with direct_dynamics, one per new parent node when factored). */
 int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
 

@@ -574,7 +574,7 @@ int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   HIPCHK(hipStreamSynchronize(s));
   int playing = 0;
   for (int v : st) playing += v == 0;
-  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing;
+  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing; out[4] = c[3];
   return MZGO_OK;
 }
 

@@ -75,8 +75,9 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // deltas per phase into mzgo_stamps[block][phase].
 // ---------------------------------------------------------------------------
 // 0-7 phases (thread 0), 8-19 per-wave conv loops, 20-31 sub-phases,
-// 32-43 per-wave conv-input work, 44-55 per-wave conv-input barrier wait
-constexpr int kStampPhases = 56;
+// 32-43 per-wave conv-input work, 44-55 per-wave conv-input barrier wait,
+// 56-63 factored simulation detail (see sim_loop)
+constexpr int kStampPhases = 64;
 #ifdef MZGO_STAMPS
 // Phase sums accumulate in LDS (a global read-modify-write per lap would put
 // an HBM round trip on the measured wave's critical path); flush() adds them
@@ -100,6 +101,7 @@ struct Stamp {
   __device__ void wave_add(int phase, unsigned long long cycles) {
     if ((threadIdx.x & 63) == 0) lds[phase] += cycles;   // one slot per wave
   }
+  __device__ unsigned long long now() const { return __builtin_amdgcn_s_memtime(); }
   __device__ void flush() {
     __syncthreads();
     if (buf && threadIdx.x < kStampPhases) buf[blockIdx.x * kStampPhases + threadIdx.x] += lds[threadIdx.x];
@@ -110,6 +112,7 @@ struct Stamp {
   __device__ explicit Stamp(unsigned long long*) {}
   __device__ void lap(int) {}
   __device__ void wave_add(int, unsigned long long) {}
+  __device__ unsigned long long now() const { return 0; }
   __device__ void flush() {}
 };
 #endif
@@ -175,6 +178,21 @@ __device__ __forceinline__ T wave_max(T v) {
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
   return wave_reduce(v, [](T a, T b) { return b < a ? b : a; });
+}
+
+// min of lo and max of hi over the wave in one interleaved pass
+template <typename T>
+__device__ __forceinline__ void wave_minmax(T& lo, T& hi) {
+  auto mn = [](T a, T b) { return b < a ? b : a; };
+  auto mx = [](T a, T b) { return b > a ? b : a; };
+  lo = mn(lo, dpp::mov<dpp::XOR1>(lo)); hi = mx(hi, dpp::mov<dpp::XOR1>(hi));
+  lo = mn(lo, dpp::mov<dpp::XOR2>(lo)); hi = mx(hi, dpp::mov<dpp::XOR2>(hi));
+  lo = mn(lo, dpp::mov<dpp::ROR4>(lo)); hi = mx(hi, dpp::mov<dpp::ROR4>(hi));
+  lo = mn(lo, dpp::mov<dpp::ROR8>(lo)); hi = mx(hi, dpp::mov<dpp::ROR8>(hi));
+  const T l0 = dpp::lane(lo, 0), l1 = dpp::lane(lo, 16), l2 = dpp::lane(lo, 32), l3 = dpp::lane(lo, 48);
+  const T h0 = dpp::lane(hi, 0), h1 = dpp::lane(hi, 16), h2 = dpp::lane(hi, 32), h3 = dpp::lane(hi, 48);
+  lo = mn(mn(l0, l1), mn(l2, l3));
+  hi = mx(mx(h0, h1), mx(h2, h3));
 }
 
 // v[i] + v[i ^ 32] and v[i] + v[i ^ 16] via the gfx950 permlane swaps

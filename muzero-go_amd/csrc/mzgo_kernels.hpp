@@ -54,7 +54,8 @@ struct EngineArrays {
   int* game_len;         // [G]
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
-  unsigned long long* counters;  // [4] 0: simulations run, 1: moves played, 2: games finished
+  unsigned long long* counters;  // [4] 0: simulations run, 1: moves played, 2: games finished,
+                                 //     3: dynamics convs run (factored: one per new parent)
   unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
 };
 
@@ -271,7 +272,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
 
   if (threadIdx.x == 0) sm.t.ycache = -1;               // the union holds no node's Y yet
   __syncthreads();
-  int nodes = 1;
+  int nodes = 1, convs = 0;
   Stamp st(E.stamps);
   for (int sim = 0; sim < S; ++sim) {
     if (wave_id() == 0) {
@@ -305,8 +306,11 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
                                             nullptr, &st);
         __syncthreads();                                 // Y stores before the expansion reads them
         yc = -1;                                         // the conv overwrote the LDS copy
+        if (threadIdx.x == 0) { st.wave_add(59, 1); ++convs; }   // convs run
       }
+      const unsigned long long t_x = st.now();
       expand_heads<G>(sm.u.f, yleaf, yc == leaf, np.etab + (size_t)a * 9 * G::C, np.head_w);
+      if (threadIdx.x == 0) st.wave_add(56, st.now() - t_x);
       __syncthreads();
       if (threadIdx.x == 0 && decltype(sm.u.f)::CACHE) sm.t.ycache = leaf;   // read by all before the barrier
       heads = sm.u.f.xh;
@@ -322,11 +326,16 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     // and (next iteration) the next select.  Wave 0 issues no HBM stores, so
     // its tree loads never wait for store acks.  The select barrier joins them.
     if (wave_id() == 1) {
+      const unsigned long long t1 = st.now();
       int* crow = TV.child + (size_t)nid * G::A;        // the new node: no children yet
       for (int i = lane_id(); i < G::A; i += 64) crow[i] = -1;   // (before its priors are published)
-      if (factored) heads_logits<G, 1>(heads, true, sm.t.hsc, sm.t.logits);
-      else heads_logits<G, Smem<G>::HEAD_PARTS>(heads, true, sm.t.hsc, sm.t.logits);
-      child_priors<G>(sm.t, TV.prior + (size_t)nid * G::A, nid, sp.variant);
+      float x[G::AP];
+      if (factored) logits_regs<G, 1>(heads, true, sm.t.hsc, x);
+      else logits_regs<G, Smem<G>::HEAD_PARTS>(heads, true, sm.t.hsc, x);
+      const unsigned long long t2 = st.now();
+      child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, nid, sp.variant);
+      st.wave_add(57, t2 - t1);
+      st.wave_add(58, st.now() - t2);
     }
     if (wave_id() == 0) {
       float r, v;
@@ -341,7 +350,11 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   __syncthreads();
   st.flush();
   tree_flush<G>(T, nodes);
-  if (threadIdx.x == 0) E.nodes[g] = nodes;
+  if (threadIdx.x == 0) {
+    E.nodes[g] = nodes;
+    // direct dynamics: one conv per expansion
+    atomicAdd(&E.counters[3], (unsigned long long)(factored ? convs : nodes - 1));
+  }
   __syncthreads();
 }
 

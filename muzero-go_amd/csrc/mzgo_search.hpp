@@ -121,19 +121,40 @@ __device__ __forceinline__ void build_mask(TreeLds<G>& t, double pass_epsilon, I
   __syncthreads();
 }
 
-// softmax over t.logits -> t.fbuf (torch CPU order: exp(x - max) * (1/sum)).
-// Wave 0 only.
+// softmax of a lane's logits x[j] (a = lane + 64*j; entries a >= A ignored)
+// -> p[j], torch CPU order: exp(x - max) * (1/sum), the per-lane partial sums
+// taken in ascending j, then the wave butterfly.  Wave-level, registers only.
+template <class G>
+__device__ __forceinline__ void softmax_regs(const float (&x)[G::AP], float (&p)[G::AP]) {
+  const int lane = lane_id_local();
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j)
+    if (lane + 64 * j < G::A) m = fmaxf(m, x[j]);
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    p[j] = lane + 64 * j < G::A ? expf(x[j] - m) : 0.f;
+    s += p[j];
+  }
+  s = wave_sum(s);
+  const float inv = 1.0f / s;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) p[j] = p[j] * inv;
+}
+
+// softmax over t.logits -> t.fbuf.  Wave 0 only.
 template <class G>
 __device__ __forceinline__ void softmax_wave(TreeLds<G>& t) {
   const int lane = lane_id_local();
-  float m = -INFINITY;
-  for (int a = lane; a < G::A; a += 64) m = fmaxf(m, t.logits[a]);
-  m = wave_max(m);
-  float s = 0.f;
-  for (int a = lane; a < G::A; a += 64) { float e = expf(t.logits[a] - m); t.fbuf[a] = e; s += e; }
-  s = wave_sum(s);
-  const float inv = 1.0f / s;
-  for (int a = lane; a < G::A; a += 64) t.fbuf[a] = t.fbuf[a] * inv;
+  float x[G::AP], p[G::AP];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) x[j] = lane + 64 * j < G::A ? t.logits[lane + 64 * j] : 0.f;
+  softmax_regs<G>(x, p);
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j)
+    if (lane + 64 * j < G::A) t.fbuf[lane + 64 * j] = p[j];
 }
 
 // Reward / value / logits from the fused head partials (self_play.py:91-94,
@@ -193,9 +214,14 @@ __device__ __forceinline__ void heads_value(const float* hp, bool has_reward, co
   const float vb = hsc[HS_VB];
   float vs = 0.f, rs = 0.f;
   const float rb = has_reward ? hsc[HS_RB] : 0.f;
-  for (int c = lane; c < G::CELLS; c += 64) {
-    vs += head_at<G, NPART>(hp, hv, c) + vb;
-    if (has_reward) rs += head_at<G, NPART>(hp, 0, c) + rb;
+  constexpr int CP = (G::CELLS + 63) / 64;
+#pragma unroll
+  for (int j = 0; j < CP; ++j) {                  // cells c = lane + 64 j, ascending per lane
+    const int c = lane + 64 * j;
+    if (c < G::CELLS) {
+      vs += head_at<G, NPART>(hp, hv, c) + vb;
+      if (has_reward) rs += head_at<G, NPART>(hp, 0, c) + rb;
+    }
   }
   vs = wave_sum(vs);
   const float vmean = vs / (float)G::CELLS;
@@ -215,14 +241,29 @@ __device__ __forceinline__ void heads_value(const float* hp, bool has_reward, co
   }
 }
 
-// policy logits (cells, then the learned pass logit).  One wave.
+// policy logits of a lane's actions a = lane + 64 j (cells, then the learned
+// pass logit), in registers.  One wave.
 template <class G, int NPART>
-__device__ __forceinline__ void heads_logits(const float* hp, bool has_reward, const float* hsc, float* logits) {
+__device__ __forceinline__ void logits_regs(const float* hp, bool has_reward, const float* hsc, float (&x)[G::AP]) {
   const int lane = lane_id_local();
   const int hpol = has_reward ? 2 : 1;
   const float pb = hsc[HS_PB];
-  for (int c = lane; c < G::CELLS; c += 64) logits[c] = head_at<G, NPART>(hp, hpol, c) + pb;
-  if (lane == 0) logits[G::CELLS] = hsc[HS_PASS];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    x[j] = a < G::CELLS ? head_at<G, NPART>(hp, hpol, a) + pb : hsc[HS_PASS];
+  }
+}
+
+// policy logits -> logits[A] (LDS).  One wave.
+template <class G, int NPART>
+__device__ __forceinline__ void heads_logits(const float* hp, bool has_reward, const float* hsc, float* logits) {
+  const int lane = lane_id_local();
+  float x[G::AP];
+  logits_regs<G, NPART>(hp, has_reward, hsc, x);
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j)
+    if (lane + 64 * j < G::A) logits[lane + 64 * j] = x[j];
 }
 
 template <class G, int NPART>
@@ -234,42 +275,53 @@ __device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward,
   if (lane_id() == 0) { *value = v; *reward = r; }
 }
 
-// Child priors of a new node (self_play.py:204-224): p = softmax * root mask,
-// normalised by numpy's f32 pairwise sum; entries with mask 0 are 0.  Wave 0.
+// Child priors of a new node (self_play.py:204-224) from its logits x (a =
+// lane + 64 j): p = softmax * root mask, normalised by numpy's f32 pairwise
+// sum; entries with mask 0 are 0.  Written to dst (HBM row) and, for a node
+// >= 0, published in t.newp for a select running concurrently on another
+// wave.  One wave; values stay in registers except for the ordered sum.
 template <class G>
-__device__ __forceinline__ void child_priors(TreeLds<G>& t, float* __restrict__ dst, int node = -1,
-                                             int variant = 0) {
+__device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::AP], float* __restrict__ dst,
+                                             int node = -1, int variant = 0) {
   const int lane = lane_id_local();
-  softmax_wave<G>(t);
+  float p[G::AP];
+  double m[G::AP];
+  softmax_regs<G>(x, p);
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) m[j] = lane + 64 * j < G::A ? mask_of<G>(t, lane + 64 * j) : 0.0;
+  float q[G::AP];
   if (variant == 1) {
     // main.py:299-309: softmax[a] where valid_mask[a] > 0, not renormalised
-    for (int a = lane; a < G::A; a += 64) {
-      const float p = mask_of<G>(t, a) > 0 ? t.fbuf[a] : 0.f;
-      dst[a] = p;
-      if (node >= 0) t.newp[a] = p;
-    }
-    if (node >= 0 && lane == 0)
-      __hip_atomic_store(&t.newp_node, node, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return;
-  }
-  for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
-  const float s = np_pairwise_sum<float, G::A>(t.fbuf);
-  if (s > 0.f) {
-    for (int a = lane; a < G::A; a += 64) {
-      const double m = mask_of<G>(t, a);
-      const float p = m > 0 ? t.fbuf[a] / s : 0.f;
-      dst[a] = p;
-      if (node >= 0) t.newp[a] = p;
-    }
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) q[j] = m[j] > 0 ? p[j] : 0.f;
   } else {
-    // fallback of :215 (uniform over the mask; the reference's f64 here is
-    // stored as f32 -- unreachable unless every valid softmax entry underflows)
-    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = mask_of<G>(t, a);
-    const double ms = np_pairwise_sum<double, G::A>(t.dbuf);
-    for (int a = lane; a < G::A; a += 64) {
-      const float p = (float)(mask_of<G>(t, a) / ms);
-      dst[a] = p;
-      if (node >= 0) t.newp[a] = p;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      p[j] = mul_f32_by_f64(p[j], m[j]);
+      if (lane + 64 * j < G::A) t.fbuf[lane + 64 * j] = p[j];
+    }
+    const float s = np_pairwise_sum<float, G::A>(t.fbuf);
+    if (s > 0.f) {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) q[j] = m[j] > 0 ? p[j] / s : 0.f;
+    } else {
+      // fallback of :215 (uniform over the mask; the reference's f64 here is
+      // stored as f32 -- unreachable unless every valid softmax entry underflows)
+      wave_lds_sync();
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j)
+        if (lane + 64 * j < G::A) t.dbuf[lane + 64 * j] = m[j];
+      const double ms = np_pairwise_sum<double, G::A>(t.dbuf);
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) q[j] = (float)(m[j] / ms);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    if (a < G::A) {
+      dst[a] = q[j];
+      if (node >= 0) t.newp[a] = q[j];
     }
   }
   // publish newp for a select running concurrently on another wave
@@ -406,28 +458,43 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         __builtin_amdgcn_s_sleep(1);
     double P[G::AP];
     int ch[G::AP];
+    // all of this node's loads first (one round trip); three sources, chosen
+    // by wave-uniform branches (a select between an LDS and a global pointer
+    // would compile to a flat load).  A fresh node has no children yet.
+    if (root) {
+      asm volatile("" ::: "memory");          // keep the LDS and HBM loads apart (no flat merge)
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        P[j] = a < G::A ? T.root_prior(a) : 0.0;
+        ch[j] = a < G::A ? T.child(0, a) : -1;
+      }
+    } else if (fresh) {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        P[j] = a < G::A ? (double)t.newp[a] : 0.0;
+        ch[j] = -1;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        P[j] = a < G::A ? (double)pr_row[a] : 0.0;
+        ch[j] = a < G::A ? T.T.child[(size_t)node * G::A + a] : -1;
+      }
+    }
+    // eligible = valid_mask[a] > 0 and prior > 0 (:255-264); every prior is 0
+    // where the root mask is (root_priors, child_priors), so prior > 0 decides
     uint64_t anypos = 0, anych = 0, elig[G::AP], unexp[G::AP];
     int n_unexp = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      const bool in = a < G::A;
-      // three sources, chosen by wave-uniform branches (a select between an LDS
-      // and a global pointer would compile to a flat load)
-      if (root) {
-        asm volatile("" ::: "memory");        // keep the LDS and HBM loads apart (no flat merge)
-        P[j] = in ? T.root_prior(a) : 0.0;
-        ch[j] = in ? T.child(0, a) : -1;
-      } else {
-        P[j] = in ? (fresh ? (double)t.newp[a] : (double)pr_row[a]) : 0.0;
-        ch[j] = in ? T.T.child[(size_t)node * G::A + a] : -1;
-      }
-      const bool pos = in && P[j] > 0.0;
-      const bool e = pos && mask_of<G>(t, a) > 0.0;
+      const bool pos = P[j] > 0.0;
       anypos |= __ballot(pos);
-      anych |= __ballot(in && ch[j] >= 0);
-      elig[j] = __ballot(e);
-      unexp[j] = __ballot(e && ch[j] < 0);
+      anych |= __ballot(ch[j] >= 0);
+      elig[j] = __ballot(pos);
+      unexp[j] = __ballot(pos && ch[j] < 0);
       n_unexp += __popcll(unexp[j]);
     }
     uint64_t any_elig = 0;
@@ -480,8 +547,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       }
     }
     if (st && root) st->lap(25);
-    lo = wave_min(lo);
-    hi = wave_max(hi);
+    wave_minmax(lo, hi);
     if (st && root) st->lap(26);
     // sqrt(max(1, N)) (self_play.py:316) or sqrt(N + 1) (main.py:354)
     const double sq = sp.variant == 1 ? sqrt((double)(nvis + 1)) : sqrt((double)(nvis > 1 ? nvis : 1));

@@ -209,10 +209,10 @@ class Engine:
         check(lib.mzgo_selfplay_inject_noise(self._h, ptr(noise)))
 
     def counters(self):
-        out = np.zeros(4, np.uint64)
+        out = np.zeros(5, np.uint64)
         check(lib.mzgo_selfplay_counters(self._h, ptr(out), stream_of(self.device)))
         return dict(simulations=int(out[0]), moves=int(out[1]), games_finished=int(out[2]),
-                    playing=int(out[3]))
+                    playing=int(out[3]), dynamics_convs=int(out[4]))
 
     def record(self, g):
         """Host copy of slot g's game record (numpy arrays)."""

@@ -73,7 +73,7 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 56), np.uint64)
+    buf = np.zeros((G, 64), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
@@ -94,6 +94,9 @@ def stamps_report():
                       "stage_detail_scatter0_transform": [round(float(v)) for v in allp[29:31]],
                       "wave_stage_work": [round(float(v)) for v in allp[32:44]],
                       "wave_stage_wait": [round(float(v)) for v in allp[44:56]],
+                      "factored_expand_pre_barrier": round(float(allp[56])),
+                      "wave1_logits": round(float(allp[57])), "wave1_priors": round(float(allp[58])),
+                      "convs_per_search": float(buf[:, 59].astype(np.float64).mean() / 2),
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 

@@ -42,6 +42,7 @@ out = {
 out["hbm_GBps"] = out["hbm_bytes_per_launch"] / (out["avg_duration_ms"] / 1e3) / 1e9
 out["tag"] = tag
 out["workload"] = sys.argv[3] if len(sys.argv) > 3 else "9x9 Go self-play, 256 parallel games/GPU, 200 sims/move"
+out["dynamics"] = sys.argv[4] if len(sys.argv) > 4 else "factored"
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
 json.dump(out, open(os.path.join(dst, "latest_summary.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
