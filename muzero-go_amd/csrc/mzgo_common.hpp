@@ -285,6 +285,19 @@ __device__ __forceinline__ T np_pairwise_sum(const T* x) {
   }
 }
 
+// position of the k-th (0-based) set bit of m (k < popcount(m)): binary search
+// on popcounts of halves
+__device__ __forceinline__ int kth_set_bit(uint64_t m, uint32_t k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t lo = m & ((1ull << w) - 1);
+    const uint32_t c = (uint32_t)__popcll(lo);
+    if (k >= c) { k -= c; m >>= w; pos += w; } else { m = lo; }
+  }
+  return pos;
+}
+
 // f32 result of numpy's in-place ``f32_array *= f64_array`` element
 __device__ __forceinline__ float mul_f32_by_f64(float p, double m) { return (float)((double)p * m); }
 

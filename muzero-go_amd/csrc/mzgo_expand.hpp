@@ -41,17 +41,30 @@ struct ExpandShape {
   static_assert(G::C % 32 == 0, "8 lanes x whole float4s per cell");
 };
 
-// LDS of the expansion: the heads, and (if they fit beside the conv buffers
-// they share a union with) a copy of one node's Y and of the 1x1 head
-// weights, so that consecutive expansions of the same leaf read them from LDS
-// instead of L2.  A conv (rare) overwrites the union; the next expansion
-// refills it.
-template <class G, bool FITS>
+// LDS of the expansion (a member of the conv union, UF floats): the heads,
+// and, if they fit, a copy of one node's Y and of the 1x1 head weights (so
+// that consecutive expansions of the same leaf read them from LDS instead of
+// L2; a conv overwrites the union and the next expansion refills it), and
+// the per-wave buffers of the batched root phase (root_batch).
+template <class G, int UF>
 struct ExpandLds {
-  static constexpr bool CACHE = FITS;
-  alignas(16) float yc[FITS ? G::CELLS * G::C : 4];
-  alignas(16) float hw[FITS ? 3 * G::C : 4];
+  static constexpr int YC = G::CELLS * G::C;
+  static constexpr int BASE = YC + 3 * G::CS + 3 * G::C;
+  static constexpr bool CACHE = BASE <= UF;
+  static constexpr int PERW = 3 * G::CS + 9 * G::C + 3 * 64 * G::AP;   // one wave's batch buffers
+  static constexpr bool BATCH = CACHE && BASE + G::WAVES * PERW + 3 * G::A + 64 <= UF;
+  alignas(16) float yc[CACHE ? YC : 4];
+  alignas(16) float hw[CACHE ? 3 * G::C : 4];
   float xh[3 * G::CS];
+  struct Wave {
+    alignas(16) float xw[3 * G::CS];      // the child's head sums
+    alignas(16) float ew[9 * G::C];       // E[a] of the child
+    float fb[64 * G::AP];                 // ordered-sum scratch (child_priors)
+    double db[64 * G::AP];
+  };
+  Wave wv[BATCH ? G::WAVES : 1];
+  double bv[BATCH ? G::A : 1];            // backup value of each batched child
+  int acts[BATCH ? G::A : 1];             // action of each batched child
 };
 
 // board region class of a cell: (row class) * 3 + (column class)
@@ -94,7 +107,19 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
     const int reg = region_of<G>(cl);
     f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
-    for (int k = 0; k < X::PERL; ++k) e[k] = E4[reg * X::C4 + j + X::LPC * k];
+    for (int k = 0; k < X::PERL; ++k) {
+#ifdef MZGO_DIAG_XNOE
+      e[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
+      e[k] = E4[reg * X::C4 + j + X::LPC * k];
+#endif
+    }
+#ifdef MZGO_DIAG_XNOY
+    if (L::CACHE && hit) {
+#pragma unroll
+      for (int k = 0; k < X::PERL; ++k) y[k] = f32x4{0.2f, 0.2f, 0.2f, 0.2f};
+    } else
+#endif
     if (L::CACHE && hit) {
 #pragma unroll
       for (int k = 0; k < X::PERL; ++k) y[k] = C4[(size_t)cl * X::C4 + j + X::LPC * k];
@@ -111,6 +136,11 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
     for (int k = 0; k < X::PERL; ++k) {
       const int c4 = j + X::LPC * k;
       f32x4 wr, wv, wp;
+#ifdef MZGO_DIAG_XNOW
+      if (true) {
+        wr = f32x4{0.1f, 0.1f, 0.1f, 0.1f}; wv = wr; wp = wr;
+      } else
+#endif
       if (lw) {
         wr = CW[c4]; wv = CW[X::C4 + c4]; wp = CW[2 * X::C4 + c4];
       } else {
@@ -135,6 +165,54 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
       lds.xh[cell] = hr;
       lds.xh[G::CS + cell] = hv;
       lds.xh[2 * G::CS + cell] = hp;
+    }
+  }
+}
+
+// One child's heads by ONE wave (the batched root phase): xw [3][CS] gets
+// the reward / value / policy sums of relu(Y + E[a]) per cell, Y [CELLS][C]
+// and E[a] [9][C] and the head weights hw [3][C] all in LDS.  Lane (j, cg):
+// channel float4s c4 = j + 8k, cells 8 pass + cg.  Wave-level; the caller
+// orders xw for the wave's readers (wave_lds_sync).
+template <class G>
+__device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw) {
+  typedef ExpandShape<G> X;
+  const int lane = lane_id_local();
+  const int j = lane & 7, cg = lane >> 3;
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(yc);
+  const f32x4* E4 = reinterpret_cast<const f32x4*>(ew);
+  const f32x4* W4 = reinterpret_cast<const f32x4*>(hw);
+  f32x4 wr[X::PERL], wv[X::PERL], wp[X::PERL];
+#pragma unroll
+  for (int k = 0; k < X::PERL; ++k) {
+    const int c4 = j + 8 * k;
+    wr[k] = W4[c4]; wv[k] = W4[X::C4 + c4]; wp[k] = W4[2 * X::C4 + c4];
+  }
+  for (int p0 = 0; p0 < G::CELLS; p0 += 8) {
+    const int cell = p0 + cg;
+    const int cl = cell < G::CELLS ? cell : G::CELLS - 1;
+    const int reg = region_of<G>(cl);
+    float hr = 0.f, hv = 0.f, hp = 0.f;
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) {
+      const int c4 = j + 8 * k;
+      const f32x4 y = Y4[cl * X::C4 + c4], e = E4[reg * X::C4 + c4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = y[q] + e[q];
+        v = v > 0.f ? v : 0.f;
+        hr = __builtin_fmaf(wr[k][q], v, hr);
+        hv = __builtin_fmaf(wv[k][q], v, hv);
+        hp = __builtin_fmaf(wp[k][q], v, hp);
+      }
+    }
+    hr = sum8(hr);
+    hv = sum8(hv);
+    hp = sum8(hp);
+    if (j == 0 && cell < G::CELLS) {
+      xw[cell] = hr;
+      xw[G::CS + cell] = hv;
+      xw[2 * G::CS + cell] = hp;
     }
   }
 }

@@ -81,7 +81,7 @@ struct Smem {
     float in[G::CINMAX * G::CPAD];                       // conv staging
     float hp[2 * 3 * G::CS];                             // head partials (after the conv loop)
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
-    ExpandLds<G, G::CELLS * G::C + 3 * G::CS + 3 * G::C <= G::CINMAX * G::CPAD> f;   // factored expansion
+    ExpandLds<G, G::CINMAX * G::CPAD> f;   // factored expansion
   } u;
   alignas(16) float ring[RingBytes<G>::value / 4];       // weight DMA ring
   TreeLds<G> t;
@@ -106,7 +106,7 @@ struct Smem<G, true> {
       alignas(16) float outs[G::C * Wino<G>::OUT_STRIDE];   // conv output staging
     } x;
     struct { int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS]; } scr;  // board step
-    ExpandLds<G, G::CELLS * G::C + 3 * G::CS + 3 * G::C <= Wino<G>::template v_floats<G::CINMAX>()> f;
+    ExpandLds<G, Wino<G>::template v_floats<G::CINMAX>()> f;
   } u;
   alignas(16) float raw[WinoRaw<G>::FLOATS];              // per-wave staging of conv input rows
   static constexpr bool STRIPS = Wino<G>::NSTRIP > 1;
@@ -255,6 +255,133 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
   return E.pool + (size_t)g * ((size_t)E.S + 2) * G::C * G::CS;
 }
 
+// Batched root phase (factored dynamics).  While the root has unexpanded
+// eligible children, select_leaf (self_play.py:283-287; main.py's select the
+// same) picks one of them by the simulation's draw alone -- no value enters
+// the choice -- so the first K = min(S, #eligible) simulations expand K
+// distinct root children in an order fixed before any of them is evaluated.
+// They run here as one batch: the root's conv once, one wave per child
+// (heads, child priors), then the K backups in simulation order, so every
+// sum is the sequential one and the tree is the same node for node.
+// Returns K (0: no batch; the simulation loop does everything).
+template <class G, class Acc>
+__device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                          const TreeView& TV, Acc& T, float* pool, float* scratch, int* nact,
+                                          uint64_t key) {
+  auto& L = sm.u.f;
+  if constexpr (!decltype(sm.u.f)::BATCH) {
+    return 0;
+  } else {
+    const int S = sp.num_simulations;
+    // eligible root children (prior > 0, as select_leaf decides)
+    if (wave_id() == 0) {
+      int n = 0;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane_id_local() + 64 * j;
+        n += __popcll(__ballot(a < G::A && T.root_prior(a) > 0.0));
+      }
+      if (lane_id() == 0) sm.t.bcast = n < S ? n : S;
+    }
+    __syncthreads();
+    const int K = sm.t.bcast;
+    if (K == 0) return 0;
+    // the root's conv Y (its latent is in the scratch slot), then Y and the
+    // head weights into LDS.  The conv overwrites the whole union, so the
+    // batch's LDS buffers are filled only after it.
+    latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
+                                        nullptr);
+    __syncthreads();
+    {
+      const f32x4* src = reinterpret_cast<const f32x4*>(pool);
+      f32x4* dst = reinterpret_cast<f32x4*>(L.yc);
+      for (int i = threadIdx.x; i < G::CELLS * G::C / 4; i += G::THREADS) dst[i] = src[i];
+      for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = np.head_w[i];
+    }
+    if (wave_id() == 0) {
+      // the simulations' choices: sim k takes the r_k-th (ascending) of the
+      // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
+      const int lane = lane_id_local();
+      uint64_t el[G::AP];
+      int n = 0;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        el[j] = __ballot(a < G::A && T.root_prior(a) > 0.0);
+        n += __popcll(el[j]);
+      }
+      uint32_t rr[G::AP];
+#pragma unroll
+      for (int m = 0; m < G::AP; ++m) {
+        const int k = lane + 64 * m;
+        rr[m] = k < K ? randbelow(draw(key, TAG_SELECT, (uint64_t)k), (uint32_t)(n - k)) : 0u;
+      }
+      for (int k = 0; k < K; ++k) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int m = 0; m < G::AP; ++m)
+          if ((k >> 6) == m) r = (uint32_t)__builtin_amdgcn_readlane((int)rr[m], k & 63);
+        int best = -1;
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j) {
+          const uint32_t c = __popcll(el[j]);
+          if (best < 0 && r < c) best = 64 * j + kth_set_bit(el[j], r);
+          else if (best < 0) r -= c;
+        }
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j)
+          if ((best >> 6) == j) el[j] &= ~(1ull << (best & 63));
+        if (lane == 0) L.acts[k] = best < 0 ? 0 : best;   // (best >= 0: r < #remaining)
+      }
+    }
+    __syncthreads();
+    // one wave per child
+    const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+    const int lane = lane_id_local();
+    auto& W = L.wv[wave];
+    for (int k = wave; k < K; k += G::WAVES) {
+      const int a = L.acts[k], nid = 1 + k;
+      const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
+      for (int i = lane; i < 9 * G::C / 4; i += 64) reinterpret_cast<f32x4*>(W.ew)[i] = e4[i];
+      wave_lds_sync();
+      expand_wave<G>(W.xw, L.yc, W.ew, L.hw);
+      wave_lds_sync();
+      float r, v, x[G::AP];
+      heads_value<G, 1>(W.xw, true, sm.t.hsc, r, v);
+      logits_regs<G, 1>(W.xw, true, sm.t.hsc, x);
+      int* crow = TV.child + (size_t)nid * G::A;
+      for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+      child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
+      if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
+      wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
+    }
+    __syncthreads();
+    if (wave_id() == 0) {
+      // the K backups of backpropagate(path + [child], v) (self_play.py:337-343)
+      for (int k = lane; k < K; k += 64) {
+        const int a = L.acts[k], nid = 1 + k;
+        const double v = L.bv[k];
+        T.init(nid);
+        T.add(nid, v);
+        T.set_child(0, a, nid);
+        T.add_root_child(a, v);
+        nact[nid] = a;
+      }
+      if (lane == 0) {
+        const bool alt = sp.variant == 0;   // main.py:366-368 does not alternate
+        for (int k = 0; k < K; ++k) {       // the root's sum in simulation order
+          const double v = L.bv[k];
+          T.add(0, alt ? -v : v);
+        }
+        sm.t.newest = -1;                    // every prior row is in HBM already
+        sm.t.ycache = 0;                     // L.yc holds the root's Y
+      }
+    }
+    __syncthreads();
+    return K;
+  }
+}
+
 // The simulations of one search with the tree accessor Acc (LDS or HBM stats).
 template <class G, class Acc>
 __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
@@ -274,7 +401,14 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   __syncthreads();
   int nodes = 1, convs = 0;
   Stamp st(E.stamps);
-  for (int sim = 0; sim < S; ++sim) {
+  int sim0 = 0;
+  if (factored) {
+    sim0 = root_batch<G, Acc>(sm, np, sp, TV, T, pool, scratch, nact, key);
+    nodes += sim0;
+    convs += sim0 > 0 ? 1 : 0;
+    st.lap(4);
+  }
+  for (int sim = sim0; sim < S; ++sim) {
     if (wave_id() == 0) {
       const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st);
       if (lane_id() == 0) sm.t.action = a;

@@ -59,6 +59,12 @@ struct TreeLds {
   int spath[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
   int rchild[G::TREE_CAP > 0 ? G::A : 1];
   double rprior[G::TREE_CAP > 0 ? G::A : 1];
+  // visit counts / value sums of the root's children, indexed by action (a
+  // mirror of svis / sws of node rchild[a]: the root's PUCT reads them in the
+  // same round trip as its priors, without a dependent gather)
+  int rvis[G::TREE_CAP > 0 ? G::A : 1];
+  double rws[G::TREE_CAP > 0 ? G::A : 1];
+  int ract;                // root action on the current simulation's path
   // priors of the newest node, written by wave 1 while wave 0 backs up and
   // selects the next leaf; select waits on newp_node only if it reaches it
   float newp[G::A];
@@ -95,7 +101,11 @@ struct TreeAcc {
   }
   __device__ __forceinline__ void set_child(int n, int a, int c) {
     T.child[(size_t)n * G::A + a] = c;
-    if constexpr (L) { if (n == 0) t.rchild[a] = c; }
+    if constexpr (L) { if (n == 0) { t.rchild[a] = c; t.rvis[a] = 0; t.rws[a] = 0.0; } }
+  }
+  // the root-child mirror: stats of the root's child a (LDS trees)
+  __device__ __forceinline__ void add_root_child(int a, double dv) {
+    if constexpr (L) { t.rvis[a] += 1; t.rws[a] = t.rws[a] + dv; }
   }
   __device__ __forceinline__ double root_prior(int a) const {
     if constexpr (L) return t.rprior[a]; else return T.root_prior[a];
@@ -280,10 +290,13 @@ __device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward,
 // sum; entries with mask 0 are 0.  Written to dst (HBM row) and, for a node
 // >= 0, published in t.newp for a select running concurrently on another
 // wave.  One wave; values stay in registers except for the ordered sum.
+// fbuf / dbuf: this wave's LDS scratch for the ordered sums (A entries each).
 template <class G>
 __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::AP], float* __restrict__ dst,
-                                             int node = -1, int variant = 0) {
+                                             int node = -1, int variant = 0, float* fbuf = nullptr,
+                                             double* dbuf = nullptr) {
   const int lane = lane_id_local();
+  if (!fbuf) { fbuf = t.fbuf; dbuf = t.dbuf; }
   float p[G::AP];
   double m[G::AP];
   softmax_regs<G>(x, p);
@@ -298,9 +311,9 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
       p[j] = mul_f32_by_f64(p[j], m[j]);
-      if (lane + 64 * j < G::A) t.fbuf[lane + 64 * j] = p[j];
+      if (lane + 64 * j < G::A) fbuf[lane + 64 * j] = p[j];
     }
-    const float s = np_pairwise_sum<float, G::A>(t.fbuf);
+    const float s = np_pairwise_sum<float, G::A>(fbuf);
     if (s > 0.f) {
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) q[j] = m[j] > 0 ? p[j] / s : 0.f;
@@ -310,8 +323,8 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::
       wave_lds_sync();
 #pragma unroll
       for (int j = 0; j < G::AP; ++j)
-        if (lane + 64 * j < G::A) t.dbuf[lane + 64 * j] = m[j];
-      const double ms = np_pairwise_sum<double, G::A>(t.dbuf);
+        if (lane + 64 * j < G::A) dbuf[lane + 64 * j] = m[j];
+      const double ms = np_pairwise_sum<double, G::A>(dbuf);
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) q[j] = (float)(m[j] / ms);
     }
@@ -456,8 +469,8 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     if (fresh)
       while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != node)
         __builtin_amdgcn_s_sleep(1);
-    double P[G::AP];
-    int ch[G::AP];
+    double P[G::AP], rw[G::AP];
+    int ch[G::AP], rn[G::AP];
     // all of this node's loads first (one round trip); three sources, chosen
     // by wave-uniform branches (a select between an LDS and a global pointer
     // would compile to a flat load).  A fresh node has no children yet.
@@ -468,6 +481,10 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         const int a = lane + 64 * j;
         P[j] = a < G::A ? T.root_prior(a) : 0.0;
         ch[j] = a < G::A ? T.child(0, a) : -1;
+        if constexpr (Acc::LDS) {
+          rn[j] = a < G::A ? t.rvis[a] : 0;
+          rw[j] = a < G::A ? t.rws[a] : 0.0;
+        }
       }
     } else if (fresh) {
 #pragma unroll
@@ -517,9 +534,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       for (int j = 0; j < G::AP; ++j) {
         const uint32_t c = __popcll(unexp[j]);
         if (best < 0 && k < c) {
-          uint64_t m = unexp[j];
-          for (uint32_t i = 0; i < k; ++i) m &= m - 1;  // drop the k lowest set bits
-          best = 64 * j + __ffsll((long long)m) - 1;
+          best = 64 * j + kth_set_bit(unexp[j], k);
         } else if (best < 0) {
           k -= c;
         }
@@ -527,6 +542,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       t.leaf = node;
       t.depth = depth;
       t.yready = anych != 0 ? 1 : 0;
+      if (root) t.ract = best;
       return best;
     }
 
@@ -540,8 +556,10 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       n[j] = 0;
       if ((elig[j] >> lane) & 1ull) {
         const int c = ch[j];
-        n[j] = T.vis(c);
-        q[j] = n[j] > 0 ? T.ws(c) / (double)n[j] : 0.0;
+        double w;
+        if (Acc::LDS && root) { n[j] = rn[j]; w = rw[j]; }     // root-child mirror (no gather)
+        else { n[j] = T.vis(c); w = T.ws(c); }
+        q[j] = n[j] > 0 ? w / (double)n[j] : 0.0;
         lo = fmin(lo, q[j]);
         hi = fmax(hi, q[j]);
       }
@@ -551,23 +569,37 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     if (st && root) st->lap(26);
     // sqrt(max(1, N)) (self_play.py:316) or sqrt(N + 1) (main.py:354)
     const double sq = sp.variant == 1 ? sqrt((double)(nvis + 1)) : sqrt((double)(nvis > 1 ? nvis : 1));
-    double best_s = -INFINITY;
-    int best_a = 0x7fffffff, best_c = -1;
+    double sc[G::AP];
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
+      sc[j] = -INFINITY;
       if ((elig[j] >> lane) & 1ull) {
         const double qn = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
         double u;
         if (root) u = ((sp.c_puct * P[j]) * sq) / (double)(1 + n[j]);
         else u = ((double)((float)sp.c_puct * (float)P[j]) * sq) / (double)(1 + n[j]);
-        const double sc = qn + u;
-        if (sc > best_s || (sc == best_s && a < best_a)) { best_s = sc; best_a = a; best_c = ch[j]; }
+        sc[j] = qn + u;
       }
     }
     if (st && root) st->lap(27);
-    wave_argmax(best_s, best_a, best_c);
+    // first strict maximum in ascending action order (:301-308): the wave's
+    // maximum score, then the lowest action holding it
+    double best_s = sc[0];
+#pragma unroll
+    for (int j = 1; j < G::AP; ++j) best_s = sc[j] > best_s ? sc[j] : best_s;
+    best_s = wave_max(best_s);
     if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return sp.variant == 1 ? -2 : -1; }
+    int best_a = -1, best_c = -1;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const uint64_t hit = __ballot(sc[j] == best_s);
+      if (best_a < 0 && hit) {
+        const int l = __ffsll((long long)hit) - 1;
+        best_a = 64 * j + l;
+        best_c = __builtin_amdgcn_readlane(ch[j], l);
+      }
+    }
+    if (root) t.ract = best_a;
     depth += 1;
     if (lane == 0) const_cast<Acc&>(T).set_path(depth, best_c);
     node = best_c;
@@ -586,10 +618,13 @@ __device__ __forceinline__ void backup(Acc& T, int depth, int nid, double v, boo
   const int lane = lane_id_local();
   const int off = nid >= 0 ? 1 : 0;
   const int count = depth + 1 + off;              // nodes on the backed-up path
+  const int ract = T.t.ract;
   for (int i = lane; i < count; i += 64) {
     const int node = (off && i == 0) ? nid : T.path(depth - (i - off));
     // self_play.py:337-343 alternates the sign; main.py:366-368 does not
-    T.add(node, (alternate && (i & 1)) ? -v : v);
+    const double dv = (alternate && (i & 1)) ? -v : v;
+    T.add(node, dv);
+    if (i == count - 2) T.add_root_child(ract, dv);   // the path's depth-1 node, by its root action
   }
   wave_lds_sync();
 }
