@@ -188,31 +188,43 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
     const int c4 = j + 8 * k;
     wr[k] = W4[c4]; wv[k] = W4[X::C4 + c4]; wp[k] = W4[2 * X::C4 + c4];
   }
-  for (int p0 = 0; p0 < G::CELLS; p0 += 8) {
-    const int cell = p0 + cg;
-    const int cl = cell < G::CELLS ? cell : G::CELLS - 1;
-    const int reg = region_of<G>(cl);
-    float hr = 0.f, hv = 0.f, hp = 0.f;
+  constexpr int U = 2;                        // passes per iteration: loads of both issued first
+  for (int p0 = 0; p0 < G::CELLS; p0 += 8 * U) {
+    f32x4 y[U][X::PERL], e[U][X::PERL];
+    int cell[U];
 #pragma unroll
-    for (int k = 0; k < X::PERL; ++k) {
-      const int c4 = j + 8 * k;
-      const f32x4 y = Y4[cl * X::C4 + c4], e = E4[reg * X::C4 + c4];
+    for (int u = 0; u < U; ++u) {
+      cell[u] = p0 + 8 * u + cg;
+      const int cl = cell[u] < G::CELLS ? cell[u] : G::CELLS - 1;
+      const int reg = region_of<G>(cl);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float v = y[q] + e[q];
-        v = v > 0.f ? v : 0.f;
-        hr = __builtin_fmaf(wr[k][q], v, hr);
-        hv = __builtin_fmaf(wv[k][q], v, hv);
-        hp = __builtin_fmaf(wp[k][q], v, hp);
+      for (int k = 0; k < X::PERL; ++k) {
+        y[u][k] = Y4[cl * X::C4 + j + 8 * k];
+        e[u][k] = E4[reg * X::C4 + j + 8 * k];
       }
     }
-    hr = sum8(hr);
-    hv = sum8(hv);
-    hp = sum8(hp);
-    if (j == 0 && cell < G::CELLS) {
-      xw[cell] = hr;
-      xw[G::CS + cell] = hv;
-      xw[2 * G::CS + cell] = hp;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float hr = 0.f, hv = 0.f, hp = 0.f;
+#pragma unroll
+      for (int k = 0; k < X::PERL; ++k) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = y[u][k][q] + e[u][k][q];
+          v = v > 0.f ? v : 0.f;
+          hr = __builtin_fmaf(wr[k][q], v, hr);
+          hv = __builtin_fmaf(wv[k][q], v, hv);
+          hp = __builtin_fmaf(wp[k][q], v, hp);
+        }
+      }
+      hr = sum8(hr);
+      hv = sum8(hv);
+      hp = sum8(hp);
+      if (j == 0 && cell[u] < G::CELLS) {
+        xw[cell[u]] = hr;
+        xw[G::CS + cell[u]] = hv;
+        xw[2 * G::CS + cell[u]] = hp;
+      }
     }
   }
 }

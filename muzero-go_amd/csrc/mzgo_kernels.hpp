@@ -255,15 +255,60 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
   return E.pool + (size_t)g * ((size_t)E.S + 2) * G::C * G::CS;
 }
 
-// Batched root phase (factored dynamics).  While the root has unexpanded
-// eligible children, select_leaf (self_play.py:283-287; main.py's select the
-// same) picks one of them by the simulation's draw alone -- no value enters
-// the choice -- so the first K = min(S, #eligible) simulations expand K
-// distinct root children in an order fixed before any of them is evaluated.
-// They run here as one batch: the root's conv once, one wave per child
-// (heads, child priors), then the K backups in simulation order, so every
-// sum is the sequential one and the tree is the same node for node.
-// Returns K (0: no batch; the simulation loop does everything).
+// Batch expansion (factored dynamics): children i < B of one parent whose Y
+// is in L.yc (and the head weights in L.hw), child i = node nid0 + i via
+// action L.acts[i]; one wave per child: E[a] into LDS, heads, the child's
+// prior row (child_priors) and child row, L.bv[i] = its backup value
+// r + discount * v.  All threads; returns synchronised.
+template <class G>
+__device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                             const TreeView& TV, int B, int nid0) {
+  auto& L = sm.u.f;
+  if constexpr (decltype(sm.u.f)::BATCH) {
+    const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+    const int lane = lane_id_local();
+    auto& W = L.wv[wave];
+    for (int k = wave; k < B; k += G::WAVES) {
+      const int a = L.acts[k], nid = nid0 + k;
+      const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
+      for (int i = lane; i < 9 * G::C / 4; i += 64) reinterpret_cast<f32x4*>(W.ew)[i] = e4[i];
+      wave_lds_sync();
+      expand_wave<G>(W.xw, L.yc, W.ew, L.hw);
+      wave_lds_sync();
+      float r, v, x[G::AP];
+      heads_value<G, 1>(W.xw, true, sm.t.hsc, r, v);
+      logits_regs<G, 1>(W.xw, true, sm.t.hsc, x);
+      int* crow = TV.child + (size_t)nid * G::A;
+      for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+      child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
+      if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
+      wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
+    }
+  }
+  __syncthreads();
+}
+
+// Node n's Y (global, [CELLS][C]) and the head weights into the LDS copies.
+// All threads; the caller synchronises.
+template <class G>
+__device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float* head_w) {
+  auto& L = sm.u.f;
+  if constexpr (decltype(sm.u.f)::CACHE) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(y);
+    f32x4* dst = reinterpret_cast<f32x4*>(L.yc);
+    for (int i = threadIdx.x; i < G::CELLS * G::C / 4; i += G::THREADS) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
+  }
+}
+
+// Batched root phase.  While the root has unexpanded eligible children,
+// select_leaf (self_play.py:283-287; main.py's select the same) picks one of
+// them by the simulation's draw alone -- no value enters the choice -- so the
+// first K = min(S, #eligible root children) simulations expand K distinct
+// root children in an order fixed before any of them is evaluated.  They run
+// as one batch: the root's conv once, batch_expand, then the K backups in
+// simulation order, so every sum is the sequential one and the tree is the
+// same node for node.  Returns K (0: no batch).
 template <class G, class Acc>
 __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                           const TreeView& TV, Acc& T, float* pool, float* scratch, int* nact,
@@ -292,12 +337,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
                                         nullptr);
     __syncthreads();
-    {
-      const f32x4* src = reinterpret_cast<const f32x4*>(pool);
-      f32x4* dst = reinterpret_cast<f32x4*>(L.yc);
-      for (int i = threadIdx.x; i < G::CELLS * G::C / 4; i += G::THREADS) dst[i] = src[i];
-      for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = np.head_w[i];
-    }
+    load_y<G>(sm, pool, np.head_w);
     if (wave_id() == 0) {
       // the simulations' choices: sim k takes the r_k-th (ascending) of the
       // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
@@ -310,53 +350,12 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         el[j] = __ballot(a < G::A && T.root_prior(a) > 0.0);
         n += __popcll(el[j]);
       }
-      uint32_t rr[G::AP];
-#pragma unroll
-      for (int m = 0; m < G::AP; ++m) {
-        const int k = lane + 64 * m;
-        rr[m] = k < K ? randbelow(draw(key, TAG_SELECT, (uint64_t)k), (uint32_t)(n - k)) : 0u;
-      }
-      for (int k = 0; k < K; ++k) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int m = 0; m < G::AP; ++m)
-          if ((k >> 6) == m) r = (uint32_t)__builtin_amdgcn_readlane((int)rr[m], k & 63);
-        int best = -1;
-#pragma unroll
-        for (int j = 0; j < G::AP; ++j) {
-          const uint32_t c = __popcll(el[j]);
-          if (best < 0 && r < c) best = 64 * j + kth_set_bit(el[j], r);
-          else if (best < 0) r -= c;
-        }
-#pragma unroll
-        for (int j = 0; j < G::AP; ++j)
-          if ((best >> 6) == j) el[j] &= ~(1ull << (best & 63));
-        if (lane == 0) L.acts[k] = best < 0 ? 0 : best;   // (best >= 0: r < #remaining)
-      }
+      pick_sequence<G>(el, n, 0, K, key, 0, L.acts);
     }
     __syncthreads();
-    // one wave per child
-    const int wave = __builtin_amdgcn_readfirstlane(wave_id());
-    const int lane = lane_id_local();
-    auto& W = L.wv[wave];
-    for (int k = wave; k < K; k += G::WAVES) {
-      const int a = L.acts[k], nid = 1 + k;
-      const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
-      for (int i = lane; i < 9 * G::C / 4; i += 64) reinterpret_cast<f32x4*>(W.ew)[i] = e4[i];
-      wave_lds_sync();
-      expand_wave<G>(W.xw, L.yc, W.ew, L.hw);
-      wave_lds_sync();
-      float r, v, x[G::AP];
-      heads_value<G, 1>(W.xw, true, sm.t.hsc, r, v);
-      logits_regs<G, 1>(W.xw, true, sm.t.hsc, x);
-      int* crow = TV.child + (size_t)nid * G::A;
-      for (int i = lane; i < G::A; i += 64) crow[i] = -1;
-      child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
-      if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
-      wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
-    }
-    __syncthreads();
+    batch_expand<G>(sm, np, sp, TV, K, 1);
     if (wave_id() == 0) {
+      const int lane = lane_id_local();
       // the K backups of backpropagate(path + [child], v) (self_play.py:337-343)
       for (int k = lane; k < K; k += 64) {
         const int a = L.acts[k], nid = 1 + k;
@@ -383,6 +382,20 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
 }
 
 // The simulations of one search with the tree accessor Acc (LDS or HBM stats).
+//
+// Factored dynamics also batch SPECULATIVELY: once a simulation's select ends
+// at a leaf with u >= 2 unexpanded eligible children, the next simulations
+// will pick further unexpanded children of the same leaf -- in an order fixed
+// by their draws -- as long as the select walk from the root reaches that
+// leaf again.  In the reference's trees it does ~99 % of the time (the same
+// depth-1 node keeps the root's PUCT maximum).  So B children of the leaf are
+// expanded as one batch (batch_expand), and wave 0 then replays the
+// simulations one by one: select from the root (exactly as the sequential
+// loop would, on the tree as it stands); if it reaches the predicted (leaf,
+// action), the precomputed child is attached and backed up; at the first
+// miss the batch's remaining children are dropped (their node ids and rows
+// are reused) and the loop continues from that select.  The tree is the
+// sequential one node for node.
 template <class G, class Acc>
 __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                          const EngineArrays& E, int g, const TreeView& TV, uint64_t key) {
@@ -392,39 +405,42 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   int* nact = E.nact + (size_t)g * ((size_t)E.S + 1);
   const int S = sp.num_simulations;
   const bool factored = sp.factored != 0;
+  constexpr bool BATCH = decltype(sm.u.f)::BATCH;
   Acc T(TV, sm.t);
   tree_reset_root<G>(T);
-  if (threadIdx.x == 0) { sm.t.newest = -1; sm.t.newp_node = -1; }
+  if (threadIdx.x == 0) { sm.t.newest = -1; sm.t.newp_node = -1; sm.t.ycache = -1; sm.t.rowc_node = -1; }
   __syncthreads();
 
-  if (threadIdx.x == 0) sm.t.ycache = -1;               // the union holds no node's Y yet
-  __syncthreads();
   int nodes = 1, convs = 0;
   Stamp st(E.stamps);
-  int sim0 = 0;
+  int sim = 0;
   if (factored) {
-    sim0 = root_batch<G, Acc>(sm, np, sp, TV, T, pool, scratch, nact, key);
-    nodes += sim0;
-    convs += sim0 > 0 ? 1 : 0;
+    sim = root_batch<G, Acc>(sm, np, sp, TV, T, pool, scratch, nact, key);
+    nodes += sim;
+    convs += sim > 0 ? 1 : 0;
     st.lap(4);
   }
-  for (int sim = sim0; sim < S; ++sim) {
-    if (wave_id() == 0) {
-      const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st);
-      if (lane_id() == 0) sm.t.action = a;
+  bool pending = false;                                   // a select for `sim` is already in sm.t
+  while (sim < S) {
+    if (!pending) {
+      if (wave_id() == 0) {
+        const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st);
+        if (lane_id() == 0) sm.t.action = a;
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    pending = false;
     st.lap(0);
     const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;
     if (a < 0) {                                         // terminal leaf: backup 0 (:188-191)
       // self_play.py: terminal leaf -> backup 0 (:188-191); main.py: nothing (:296)
       if (wave_id() == 0 && a == -1) backup<G>(T, depth, -1, 0.0);
       __syncthreads();
+      ++sim;
       continue;
     }
-    const int nid = nodes++;
-    if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
     const float* heads;
+    const int nid = nodes;
     if (factored) {
       // the leaf's conv Y exists once it has a child; otherwise compute it now
       // (from its latent, rebuilt from its parent's Y unless it is the root)
@@ -442,6 +458,120 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         yc = -1;                                         // the conv overwrote the LDS copy
         if (threadIdx.x == 0) { st.wave_add(59, 1); ++convs; }   // convs run
       }
+      const int nun = sm.t.nunexp;
+      const int B = BATCH ? (nun < S - sim ? nun : S - sim) : 1;
+      if (BATCH && B >= 2) {
+        // ---- speculative batch of B children of `leaf` ----
+        if (yc != leaf) load_y<G>(sm, yleaf, np.head_w);
+        if constexpr (Acc::LDS) {
+          if (leaf != 0 && sm.t.rowc_node != leaf) {      // the replay's selects read leaf's rows from LDS
+            for (int i = threadIdx.x; i < G::A; i += G::THREADS) {
+              sm.t.rowc_child[i] = TV.child[(size_t)leaf * G::A + i];
+              sm.t.rowc_prior[i] = TV.prior[(size_t)leaf * G::A + i];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) sm.t.rowc_node = leaf;
+          }
+        }
+        if (wave_id() == 0) {
+          uint64_t um[G::AP];
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) um[j] = sm.t.umask[j];
+          if (lane_id() == 0) sm.u.f.acts[0] = a;
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j)
+            if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
+          pick_sequence<G>(um, nun - 1, 0, B - 1, key, sim + 1, sm.u.f.acts + 1);
+        }
+        __syncthreads();
+        batch_expand<G>(sm, np, sp, TV, B, nid);
+        st.lap(5);
+        if (wave_id() == 0) {
+          const int lane = lane_id_local();
+          if (lane == 0) { sm.t.newest = -1; sm.t.ycache = leaf; }
+          wave_lds_sync();
+          int m = 0;
+          const bool alt = sp.variant == 0;
+          if (Acc::LDS && depth == 1) {
+            // the common case: the leaf is a root child.  Simulation sim + i's
+            // select walks root -> leaf iff the root's PUCT picks the leaf's
+            // action, and then picks acts[i] there (its draw, by construction).
+            // The root's child stats are held in registers (the LDS mirror,
+            // updated with the same operations) and only its PUCT is re-run.
+            const int ac = sm.t.ract;
+            double P[G::AP], w[G::AP];
+            int n[G::AP], ch[G::AP];
+            uint64_t elig[G::AP], unexp = 0;
+#pragma unroll
+            for (int j = 0; j < G::AP; ++j) {
+              const int a2 = lane + 64 * j;
+              const bool in = a2 < G::A;
+              P[j] = in ? T.root_prior(a2) : 0.0;
+              ch[j] = in ? T.child(0, a2) : -1;
+              n[j] = in ? sm.t.rvis[a2] : 0;
+              w[j] = in ? sm.t.rws[a2] : 0.0;
+              elig[j] = __ballot(P[j] > 0.0);
+              unexp |= __ballot(P[j] > 0.0 && ch[j] < 0);
+            }
+            int nroot = T.vis(0);
+            for (int i = 0; i < B; ++i) {
+              const int ai = sm.u.f.acts[i];
+              if (i > 0) {
+                bool ok = unexp == 0;                  // else select takes an unexpanded root child
+                if (ok) {
+                  int bc;
+                  ok = puct_pick<G>(P, n, w, elig, ch, nroot, true, sp, bc) == ac;
+                }
+                if (!ok) {                             // the walk leaves the batch
+                  const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, nullptr);
+                  if (lane == 0) sm.t.action = a2;
+                  break;
+                }
+              }
+              const int n2 = nid + i;
+              if (lane == 0) { T.init(n2); nact[n2] = ai; }
+              if (lane == (ai & 63)) T.set_child(leaf, ai, n2);
+              const double v = sm.u.f.bv[i];
+              backup<G>(T, 1, n2, v, alt);
+              const double dvc = alt ? -v : v;         // the leaf's (depth 1) share
+#pragma unroll
+              for (int j = 0; j < G::AP; ++j)
+                if (lane == (ac & 63) && j == (ac >> 6)) { n[j] += 1; w[j] = w[j] + dvc; }
+              nroot += 1;
+              ++m;
+            }
+          } else {
+            for (int i = 0; i < B; ++i) {
+              const int ai = sm.u.f.acts[i];
+              if (i > 0) {
+                const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, nullptr);
+                if (a2 != ai || sm.t.leaf != leaf) {           // prediction ends: a2 is sim + i's select
+                  if (lane == 0) sm.t.action = a2;
+                  break;
+                }
+              }
+              const int n2 = nid + i;
+              if (lane == 0) { T.init(n2); nact[n2] = ai; }
+              if (lane == (ai & 63)) T.set_child(leaf, ai, n2);
+              // the next select reads leaf's child row: from LDS (rowc) on LDS
+              // trees; otherwise let the HBM store land first
+              if constexpr (!Acc::LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              backup<G>(T, depth, n2, sm.u.f.bv[i], alt);
+              ++m;
+            }
+          }
+          if (lane == 0) sm.t.bcast = m;
+        }
+        __syncthreads();
+        const int m = sm.t.bcast;
+        nodes += m;
+        sim += m;
+        pending = m < B;
+        st.lap(3);
+        continue;
+      }
+      // ---- one expansion ----
+      if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
       const unsigned long long t_x = st.now();
       expand_heads<G>(sm.u.f, yleaf, yc == leaf, np.etab + (size_t)a * 9 * G::C, np.head_w);
       if (threadIdx.x == 0) st.wave_add(56, st.now() - t_x);
@@ -449,11 +579,13 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       if (threadIdx.x == 0 && decltype(sm.u.f)::CACHE) sm.t.ycache = leaf;   // read by all before the barrier
       heads = sm.u.f.xh;
     } else {
+      if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
       latent_conv<G, G::C, G::C, 3>(sm, np.w_dyn, np.b_dyn, pool + (size_t)leaf * node_floats, G::CS,
                                     np.emb + (size_t)a * G::C, pool + (size_t)nid * node_floats, G::CS, G::CS,
                                     np.head_w, &st);
       heads = sm.heads();
     }
+    nodes += 1;
     st.lap(2);
     // wave 1: policy logits -> the new node's priors (published in LDS for a
     // select that reaches it); wave 0, meanwhile: value/reward heads, backup
@@ -480,6 +612,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       backup<G>(T, depth, nid, (double)r + sp.discount * (double)v, sp.variant == 0);
     }
     st.lap(3);
+    ++sim;
   }
   __syncthreads();
   st.flush();

@@ -51,6 +51,8 @@ struct TreeLds {
   float reward, value;
   int leaf, action, nid, depth, nodes, bcast;
   int yready;              // select's leaf already has a child (its conv Y exists: factored mode)
+  int nunexp;              // select's leaf: number of unexpanded eligible children
+  uint64_t umask[G::AP];   //   and their bitmask (a = 64 j + bit), the chosen one included
   int ycache;              // node whose Y the LDS copy holds (factored mode), -1: none
   float hsc[64];                   // staged HeadScalars (HS_* offsets)
   // LDS-resident tree state (boards with G::TREE_CAP > 0 and S + 2 <= TREE_CAP)
@@ -65,6 +67,11 @@ struct TreeLds {
   int rvis[G::TREE_CAP > 0 ? G::A : 1];
   double rws[G::TREE_CAP > 0 ? G::A : 1];
   int ract;                // root action on the current simulation's path
+  // LDS copy of one non-root node's prior row and child row (the leaf of a
+  // speculative batch, whose child row the batch's replay keeps updating)
+  int rowc_node;           // -1: none
+  int rowc_child[G::TREE_CAP > 0 ? G::A : 1];
+  float rowc_prior[G::TREE_CAP > 0 ? G::A : 1];
   // priors of the newest node, written by wave 1 while wave 0 backs up and
   // selects the next leaf; select waits on newp_node only if it reaches it
   float newp[G::A];
@@ -101,7 +108,10 @@ struct TreeAcc {
   }
   __device__ __forceinline__ void set_child(int n, int a, int c) {
     T.child[(size_t)n * G::A + a] = c;
-    if constexpr (L) { if (n == 0) { t.rchild[a] = c; t.rvis[a] = 0; t.rws[a] = 0.0; } }
+    if constexpr (L) {
+      if (n == 0) { t.rchild[a] = c; t.rvis[a] = 0; t.rws[a] = 0.0; }
+      else if (n == t.rowc_node) t.rowc_child[a] = c;
+    }
   }
   // the root-child mirror: stats of the root's child a (LDS trees)
   __device__ __forceinline__ void add_root_child(int a, double dv) {
@@ -450,6 +460,102 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
   }
 }
 
+// The choices of simulations sim0, sim0 + 1, ... (count of them) that each
+// take an unexpanded eligible child of the same node: simulation sim0 + i
+// picks the r-th (ascending) of the n - i still unexpanded ones (bitmask m),
+// r = randbelow(draw(key, TAG_SELECT, sim0 + i), n - i) -- select_leaf's
+// random.choice (self_play.py:283-287) replayed.  out[i] (LDS) gets the
+// action.  Wave-level (wave-uniform results); m is updated.
+template <class G>
+__device__ __forceinline__ void pick_sequence(uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
+                                              int sim0, int* out) {
+  const int lane = lane_id_local();
+  uint32_t rr[G::AP];
+#pragma unroll
+  for (int q = 0; q < G::AP; ++q) {              // the draws in parallel, lane i = i0 + lane + 64 q
+    const int i = lane + 64 * q;
+    rr[q] = i < count ? randbelow(draw(key, TAG_SELECT, (uint64_t)(sim0 + i)), (uint32_t)(n - i)) : 0u;
+  }
+  for (int i = 0; i < count; ++i) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < G::AP; ++q)
+      if ((i >> 6) == q) r = (uint32_t)__builtin_amdgcn_readlane((int)rr[q], i & 63);
+    int best = -1;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const uint32_t c = __popcll(m[j]);
+      if (best < 0 && r < c) best = 64 * j + kth_set_bit(m[j], r);
+      else if (best < 0) r -= c;
+    }
+    if (best < 0) best = 0;                      // unreachable: r < n - i = popcount(m)
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if ((best >> 6) == j) m[j] &= ~(1ull << (best & 63));
+    if (lane == 0) out[i0 + i] = best;
+  }
+}
+
+// PUCT over the eligible, all expanded children elig (self_play.py:290-308;
+// main.py:338-364): q = W/N min-max normalised over them, u = c_puct * P *
+// sqrt(max(1, N_parent)) / (1 + n) (main.py: sqrt(N_parent + 1)); root priors
+// f64, child priors f32 with an f32 c_puct * P (NEP 50); the first strict
+// maximum in ascending action order.  Returns the action (-1: no finite
+// score) and, in best_c, its child id.  Wave-level.
+template <class G>
+__device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n)[G::AP], const double (&w)[G::AP],
+                                         const uint64_t (&elig)[G::AP], const int (&ch)[G::AP], int nvis,
+                                         bool root, const SearchParams& sp, int& best_c, Stamp* st = nullptr) {
+  const int lane = lane_id_local();
+  double q[G::AP];
+  double lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    q[j] = 0.0;
+    if ((elig[j] >> lane) & 1ull) {
+      q[j] = n[j] > 0 ? w[j] / (double)n[j] : 0.0;
+      lo = fmin(lo, q[j]);
+      hi = fmax(hi, q[j]);
+    }
+  }
+  if (st) st->lap(25);
+  wave_minmax(lo, hi);
+  if (st) st->lap(26);
+  // sqrt(max(1, N)) (self_play.py:316) or sqrt(N + 1) (main.py:354)
+  const double sq = sp.variant == 1 ? sqrt((double)(nvis + 1)) : sqrt((double)(nvis > 1 ? nvis : 1));
+  double sc[G::AP];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    sc[j] = -INFINITY;
+    if ((elig[j] >> lane) & 1ull) {
+      const double qn = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
+      double u;
+      if (root) u = ((sp.c_puct * P[j]) * sq) / (double)(1 + n[j]);
+      else u = ((double)((float)sp.c_puct * (float)P[j]) * sq) / (double)(1 + n[j]);
+      sc[j] = qn + u;
+    }
+  }
+  if (st) st->lap(27);
+  // the wave's maximum score, then the lowest action holding it
+  double best_s = sc[0];
+#pragma unroll
+  for (int j = 1; j < G::AP; ++j) best_s = sc[j] > best_s ? sc[j] : best_s;
+  best_s = wave_max(best_s);
+  best_c = -1;
+  if (!(best_s > -INFINITY)) return -1;
+  int best_a = -1;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const uint64_t hit = __ballot(sc[j] == best_s);
+    if (best_a < 0 && hit) {
+      const int l = __ffsll((long long)hit) - 1;
+      best_a = 64 * j + l;
+      best_c = __builtin_amdgcn_readlane(ch[j], l);
+    }
+  }
+  return best_a;
+}
+
 // ---------------------------------------------------------------------------
 // select_leaf (self_play.py:239-335).  Wave 0.  Returns the action to expand
 // at t.leaf, or -1 when the walk ends at a terminal node (t.leaf).  The path
@@ -492,6 +598,13 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         const int a = lane + 64 * j;
         P[j] = a < G::A ? (double)t.newp[a] : 0.0;
         ch[j] = -1;
+      }
+    } else if (Acc::LDS && node == t.rowc_node) {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        P[j] = a < G::A ? (double)t.rowc_prior[a] : 0.0;
+        ch[j] = a < G::A ? t.rowc_child[a] : -1;
       }
     } else {
 #pragma unroll
@@ -542,63 +655,28 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
       t.leaf = node;
       t.depth = depth;
       t.yready = anych != 0 ? 1 : 0;
+      t.nunexp = n_unexp;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) t.umask[j] = unexp[j];
       if (root) t.ract = best;
       return best;
     }
 
     // PUCT over the (all expanded) eligible children
-    double q[G::AP];
     int n[G::AP];
-    double lo = INFINITY, hi = -INFINITY;
+    double w[G::AP];
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      q[j] = 0.0;
       n[j] = 0;
+      w[j] = 0.0;
       if ((elig[j] >> lane) & 1ull) {
-        const int c = ch[j];
-        double w;
-        if (Acc::LDS && root) { n[j] = rn[j]; w = rw[j]; }     // root-child mirror (no gather)
-        else { n[j] = T.vis(c); w = T.ws(c); }
-        q[j] = n[j] > 0 ? w / (double)n[j] : 0.0;
-        lo = fmin(lo, q[j]);
-        hi = fmax(hi, q[j]);
+        if (Acc::LDS && root) { n[j] = rn[j]; w[j] = rw[j]; }     // root-child mirror (no gather)
+        else { n[j] = T.vis(ch[j]); w[j] = T.ws(ch[j]); }
       }
     }
-    if (st && root) st->lap(25);
-    wave_minmax(lo, hi);
-    if (st && root) st->lap(26);
-    // sqrt(max(1, N)) (self_play.py:316) or sqrt(N + 1) (main.py:354)
-    const double sq = sp.variant == 1 ? sqrt((double)(nvis + 1)) : sqrt((double)(nvis > 1 ? nvis : 1));
-    double sc[G::AP];
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      sc[j] = -INFINITY;
-      if ((elig[j] >> lane) & 1ull) {
-        const double qn = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
-        double u;
-        if (root) u = ((sp.c_puct * P[j]) * sq) / (double)(1 + n[j]);
-        else u = ((double)((float)sp.c_puct * (float)P[j]) * sq) / (double)(1 + n[j]);
-        sc[j] = qn + u;
-      }
-    }
-    if (st && root) st->lap(27);
-    // first strict maximum in ascending action order (:301-308): the wave's
-    // maximum score, then the lowest action holding it
-    double best_s = sc[0];
-#pragma unroll
-    for (int j = 1; j < G::AP; ++j) best_s = sc[j] > best_s ? sc[j] : best_s;
-    best_s = wave_max(best_s);
-    if (!(best_s > -INFINITY)) { t.leaf = node; t.depth = depth; return sp.variant == 1 ? -2 : -1; }
-    int best_a = -1, best_c = -1;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const uint64_t hit = __ballot(sc[j] == best_s);
-      if (best_a < 0 && hit) {
-        const int l = __ffsll((long long)hit) - 1;
-        best_a = 64 * j + l;
-        best_c = __builtin_amdgcn_readlane(ch[j], l);
-      }
-    }
+    int best_c = -1;
+    const int best_a = puct_pick<G>(P, n, w, elig, ch, nvis, root, sp, best_c, root ? st : nullptr);
+    if (best_a < 0) { t.leaf = node; t.depth = depth; return sp.variant == 1 ? -2 : -1; }
     if (root) t.ract = best_a;
     depth += 1;
     if (lane == 0) const_cast<Acc&>(T).set_path(depth, best_c);

@@ -96,6 +96,8 @@ def stamps_report():
                       "wave_stage_wait": [round(float(v)) for v in allp[44:56]],
                       "factored_expand_pre_barrier": round(float(allp[56])),
                       "wave1_logits": round(float(allp[57])), "wave1_priors": round(float(allp[58])),
+                      "replay_select_to_accept": round(float(allp[60])), "replay_init_setchild": round(float(allp[61])),
+                      "replay_backup": round(float(allp[62])),
                       "convs_per_search": float(buf[:, 59].astype(np.float64).mean() / 2),
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
