@@ -205,21 +205,24 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float hr = 0.f, hv = 0.f, hp = 0.f;
+      // channel pairs in packed f32 (v_pk_add / v_pk_fma: two channels per
+      // instruction), two partial sums per head
+      f32x2 hr2 = {0.f, 0.f}, hv2 = {0.f, 0.f}, hp2 = {0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < X::PERL; ++k) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v = y[u][k][q] + e[u][k][q];
-          v = v > 0.f ? v : 0.f;
-          hr = __builtin_fmaf(wr[k][q], v, hr);
-          hv = __builtin_fmaf(wv[k][q], v, hv);
-          hp = __builtin_fmaf(wp[k][q], v, hp);
+        for (int q = 0; q < 4; q += 2) {
+          f32x2 v = f32x2{y[u][k][q], y[u][k][q + 1]} + f32x2{e[u][k][q], e[u][k][q + 1]};
+          v.x = v.x > 0.f ? v.x : 0.f;
+          v.y = v.y > 0.f ? v.y : 0.f;
+          hr2 = __builtin_elementwise_fma(f32x2{wr[k][q], wr[k][q + 1]}, v, hr2);
+          hv2 = __builtin_elementwise_fma(f32x2{wv[k][q], wv[k][q + 1]}, v, hv2);
+          hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
         }
       }
-      hr = sum8(hr);
-      hv = sum8(hv);
-      hp = sum8(hp);
+      float hr = sum8(hr2.x + hr2.y);
+      float hv = sum8(hv2.x + hv2.y);
+      float hp = sum8(hp2.x + hp2.y);
       if (j == 0 && cell[u] < G::CELLS) {
         xw[cell[u]] = hr;
         xw[G::CS + cell[u]] = hv;
@@ -231,18 +234,32 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
 
 // The latent of a node that is about to become a parent: relu(Y_par + E[a])
 // -> dst [C][CS] (channel-major, pad cells 0), the layout the 3x3 conv reads.
-// All threads; the caller synchronises before the conv reads dst.
+// Y is cell-major, so 32-channel slabs are transposed through LDS (lds: at
+// least 32 * (CS + 1) floats, free until the conv): coalesced reads and
+// writes.  All threads; returns synchronised.
 template <class G>
 __device__ __forceinline__ void materialize(float* __restrict__ dst, const float* __restrict__ Ypar,
-                                            const float* __restrict__ ea) {
-  for (int i = threadIdx.x; i < G::C * G::CS; i += G::THREADS) {
-    const int c = i / G::CS, p = i - c * G::CS;
-    float v = 0.f;
-    if (p < G::CELLS) {
-      v = Ypar[(size_t)p * G::C + c] + ea[region_of<G>(p) * G::C + c];
-      v = v > 0.f ? v : 0.f;
+                                            const float* __restrict__ ea, float* lds) {
+  constexpr int CB = 32, CSP = G::CS + 1, C4 = G::C / 4;
+  static_assert(G::C % CB == 0, "32-channel slabs");
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(Ypar);
+  const f32x4* E4 = reinterpret_cast<const f32x4*>(ea);
+  for (int c0 = 0; c0 < G::C; c0 += CB) {
+    for (int i = threadIdx.x; i < G::CELLS * (CB / 4); i += G::THREADS) {
+      const int p = i / (CB / 4), q = i - p * (CB / 4);
+      const f32x4 y = Y4[p * C4 + c0 / 4 + q], e = E4[region_of<G>(p) * C4 + c0 / 4 + q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = y[k] + e[k];
+        lds[(4 * q + k) * CSP + p] = v > 0.f ? v : 0.f;
+      }
     }
-    dst[i] = v;
+    __syncthreads();
+    for (int i = threadIdx.x; i < CB * G::CS; i += G::THREADS) {
+      const int c = i / G::CS, p = i - c * G::CS;
+      dst[(size_t)(c0 + c) * G::CS + p] = p < G::CELLS ? lds[c * CSP + p] : 0.f;
+    }
+    __syncthreads();
   }
 }
 

@@ -91,6 +91,7 @@ struct Smem {
   int misc[8];
   int bc[8];                                             // broadcast slots
   __device__ float* heads() { return u.hp; }
+  __device__ float* ulds() { return u.in; }             // the union as scratch
   static constexpr int HEAD_PARTS = ConvShape<G::C>::NCOG;
 };
 
@@ -118,6 +119,7 @@ struct Smem<G, true> {
   int misc[8];
   int bc[8];
   __device__ float* heads() { return STRIPS ? hfin : u.x.hp; }
+  __device__ float* ulds() { return u.v; }              // the union as scratch
   static constexpr int HEAD_PARTS = STRIPS ? 1 : G::C / 16;
 };
 
@@ -259,33 +261,42 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
 // is in L.yc (and the head weights in L.hw), child i = node nid0 + i via
 // action L.acts[i]; one wave per child: E[a] into LDS, heads, the child's
 // prior row (child_priors) and child row, L.bv[i] = its backup value
-// r + discount * v.  All threads; returns synchronised.
+// r + discount * v.  Waves 1.. take the children; wave 0 publishes the
+// actions meanwhile (pick_sequence, sm.t.npick) and returns at once.  All
+// threads; the caller synchronises.
 template <class G>
 __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
-                                             const TreeView& TV, int B, int nid0) {
+                                             const TreeView& TV, int B, int nid0, Stamp* st = nullptr) {
   auto& L = sm.u.f;
   if constexpr (decltype(sm.u.f)::BATCH) {
     const int wave = __builtin_amdgcn_readfirstlane(wave_id());
     const int lane = lane_id_local();
+    if (wave == 0) return;
     auto& W = L.wv[wave];
-    for (int k = wave; k < B; k += G::WAVES) {
+    for (int k = wave - 1; k < B; k += G::WAVES - 1) {
+      while (__hip_atomic_load(&sm.t.npick, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
+        __builtin_amdgcn_s_sleep(2);
       const int a = L.acts[k], nid = nid0 + k;
       const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
+      if (st) st->lap(64);
       for (int i = lane; i < 9 * G::C / 4; i += 64) reinterpret_cast<f32x4*>(W.ew)[i] = e4[i];
       wave_lds_sync();
+      if (st) st->lap(65);
       expand_wave<G>(W.xw, L.yc, W.ew, L.hw);
       wave_lds_sync();
+      if (st) st->lap(66);
       float r, v, x[G::AP];
       heads_value<G, 1>(W.xw, true, sm.t.hsc, r, v);
       logits_regs<G, 1>(W.xw, true, sm.t.hsc, x);
       int* crow = TV.child + (size_t)nid * G::A;
       for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+      if (st) st->lap(67);
       child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
       if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
       wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
+      if (st) st->lap(68);
     }
   }
-  __syncthreads();
 }
 
 // Node n's Y (global, [CELLS][C]) and the head weights into the LDS copies.
@@ -338,6 +349,8 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
                                         nullptr);
     __syncthreads();
     load_y<G>(sm, pool, np.head_w);
+    if (threadIdx.x == 0) sm.t.npick = 0;
+    __syncthreads();
     if (wave_id() == 0) {
       // the simulations' choices: sim k takes the r_k-th (ascending) of the
       // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
@@ -350,10 +363,10 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         el[j] = __ballot(a < G::A && T.root_prior(a) > 0.0);
         n += __popcll(el[j]);
       }
-      pick_sequence<G>(el, n, 0, K, key, 0, L.acts);
+      pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick);
     }
-    __syncthreads();
     batch_expand<G>(sm, np, sp, TV, K, 1);
+    __syncthreads();
     if (wave_id() == 0) {
       const int lane = lane_id_local();
       // the K backups of backpropagate(path + [child], v) (self_play.py:337-343)
@@ -449,8 +462,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       if (!sm.t.yready) {
         if (leaf != 0) {
           const int par = T.path(depth - 1);
-          materialize<G>(scratch, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C);
-          __syncthreads();
+          materialize<G>(scratch, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
+                         sm.ulds());
         }
         latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS, G::CS,
                                             nullptr, &st);
@@ -462,6 +475,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       const int B = BATCH ? (nun < S - sim ? nun : S - sim) : 1;
       if (BATCH && B >= 2) {
         // ---- speculative batch of B children of `leaf` ----
+        st.lap(69);
         if (yc != leaf) load_y<G>(sm, yleaf, np.head_w);
         if constexpr (Acc::LDS) {
           if (leaf != 0 && sm.t.rowc_node != leaf) {      // the replay's selects read leaf's rows from LDS
@@ -473,18 +487,21 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
             if (threadIdx.x == 0) sm.t.rowc_node = leaf;
           }
         }
+        if (threadIdx.x == 0) { sm.u.f.acts[0] = a; sm.t.npick = 1; }
+        __syncthreads();
+        st.lap(70);
         if (wave_id() == 0) {
           uint64_t um[G::AP];
 #pragma unroll
           for (int j = 0; j < G::AP; ++j) um[j] = sm.t.umask[j];
-          if (lane_id() == 0) sm.u.f.acts[0] = a;
 #pragma unroll
           for (int j = 0; j < G::AP; ++j)
             if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
-          pick_sequence<G>(um, nun - 1, 0, B - 1, key, sim + 1, sm.u.f.acts + 1);
+          pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick);
+          st.lap(71);
         }
+        batch_expand<G>(sm, np, sp, TV, B, nid, &st);
         __syncthreads();
-        batch_expand<G>(sm, np, sp, TV, B, nid);
         st.lap(5);
         if (wave_id() == 0) {
           const int lane = lane_id_local();
@@ -520,19 +537,23 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
                 bool ok = unexp == 0;                  // else select takes an unexpanded root child
                 if (ok) {
                   int bc;
-                  ok = puct_pick<G>(P, n, w, elig, ch, nroot, true, sp, bc) == ac;
+                  ok = puct_pick<G>(P, n, w, elig, ch, nroot, true, sp, bc, &st) == ac;
                 }
                 if (!ok) {                             // the walk leaves the batch
-                  const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, nullptr);
+                  st.lap(30);
+                  const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, &st);
                   if (lane == 0) sm.t.action = a2;
                   break;
                 }
               }
               const int n2 = nid + i;
+              st.lap(60);
               if (lane == 0) { T.init(n2); nact[n2] = ai; }
               if (lane == (ai & 63)) T.set_child(leaf, ai, n2);
               const double v = sm.u.f.bv[i];
+              st.lap(61);
               backup<G>(T, 1, n2, v, alt);
+              st.lap(62);
               const double dvc = alt ? -v : v;         // the leaf's (depth 1) share
 #pragma unroll
               for (int j = 0; j < G::AP; ++j)
@@ -544,7 +565,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
             for (int i = 0; i < B; ++i) {
               const int ai = sm.u.f.acts[i];
               if (i > 0) {
-                const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, nullptr);
+                const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, &st);
                 if (a2 != ai || sm.t.leaf != leaf) {           // prediction ends: a2 is sim + i's select
                   if (lane == 0) sm.t.action = a2;
                   break;
@@ -567,7 +588,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         nodes += m;
         sim += m;
         pending = m < B;
-        st.lap(3);
+        st.lap(63);
+        if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
         continue;
       }
       // ---- one expansion ----

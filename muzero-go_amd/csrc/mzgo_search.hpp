@@ -51,6 +51,7 @@ struct TreeLds {
   float reward, value;
   int leaf, action, nid, depth, nodes, bcast;
   int yready;              // select's leaf already has a child (its conv Y exists: factored mode)
+  int npick;               // batch actions published so far (pick_sequence -> batch_expand)
   int nunexp;              // select's leaf: number of unexpanded eligible children
   uint64_t umask[G::AP];   //   and their bitmask (a = 64 j + bit), the chosen one included
   int ycache;              // node whose Y the LDS copy holds (factored mode), -1: none
@@ -464,17 +465,26 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 // take an unexpanded eligible child of the same node: simulation sim0 + i
 // picks the r-th (ascending) of the n - i still unexpanded ones (bitmask m),
 // r = randbelow(draw(key, TAG_SELECT, sim0 + i), n - i) -- select_leaf's
-// random.choice (self_play.py:283-287) replayed.  out[i] (LDS) gets the
-// action.  Wave-level (wave-uniform results); m is updated.
+// random.choice (self_play.py:283-287) replayed.  out[i0 + i] (LDS) gets
+// the action, and *progress (LDS, if given) the number published so far.
+// Wave-level (wave-uniform results); m is updated.
 template <class G>
 __device__ __forceinline__ void pick_sequence(uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
-                                              int sim0, int* out) {
+                                              int sim0, int* out, int* progress = nullptr) {
   const int lane = lane_id_local();
   uint32_t rr[G::AP];
 #pragma unroll
-  for (int q = 0; q < G::AP; ++q) {              // the draws in parallel, lane i = i0 + lane + 64 q
+  for (int q = 0; q < G::AP; ++q) {              // the draws in parallel, lane i = lane + 64 q
     const int i = lane + 64 * q;
     rr[q] = i < count ? randbelow(draw(key, TAG_SELECT, (uint64_t)(sim0 + i)), (uint32_t)(n - i)) : 0u;
+  }
+  // the masks as scalars (wave-uniform): the serial picks run on the SALU
+  uint64_t ms[G::AP];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m[j]);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m[j] >> 32));
+    ms[j] = ((uint64_t)hi << 32) | lo;
   }
   for (int i = 0; i < count; ++i) {
     uint32_t r = 0;
@@ -484,16 +494,22 @@ __device__ __forceinline__ void pick_sequence(uint64_t (&m)[G::AP], int n, int i
     int best = -1;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const uint32_t c = __popcll(m[j]);
-      if (best < 0 && r < c) best = 64 * j + kth_set_bit(m[j], r);
+      const uint32_t c = __popcll(ms[j]);
+      if (best < 0 && r < c) best = 64 * j + kth_set_bit(ms[j], r);
       else if (best < 0) r -= c;
     }
     if (best < 0) best = 0;                      // unreachable: r < n - i = popcount(m)
 #pragma unroll
     for (int j = 0; j < G::AP; ++j)
-      if ((best >> 6) == j) m[j] &= ~(1ull << (best & 63));
-    if (lane == 0) out[i0 + i] = best;
+      if ((best >> 6) == j) ms[j] &= ~(1ull << (best & 63));
+    if (lane == 0) {
+      out[i0 + i] = best;
+      // published as soon as made: batch_expand's waves start on their children
+      if (progress) __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) m[j] = ms[j];
 }
 
 // PUCT over the eligible, all expanded children elig (self_play.py:290-308;

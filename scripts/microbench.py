@@ -73,7 +73,7 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 64), np.uint64)
+    buf = np.zeros((G, 72), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
@@ -98,6 +98,12 @@ def stamps_report():
                       "wave1_logits": round(float(allp[57])), "wave1_priors": round(float(allp[58])),
                       "replay_select_to_accept": round(float(allp[60])), "replay_init_setchild": round(float(allp[61])),
                       "replay_backup": round(float(allp[62])),
+                      "batch_end_barrier_total": round(float(allp[63]) * 2 * S / 2),
+                      "batches_per_search": float(buf[:, 31].astype(np.float64).mean() / 2),
+                      "batched_sims_per_search": float(buf[:, 28].astype(np.float64).mean() / 2),
+                      "batch_detail_total_w0": [round(float(v) * S) for v in allp[64:72]],
+                      "conv_slots_total": [round(float(allp[i]) * S) for i in (1, 6, 7, 20, 21, 29, 30)],
+                      "slot3_total": round(float(allp[3]) * S),
                       "convs_per_search": float(buf[:, 59].astype(np.float64).mean() / 2),
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
