@@ -509,36 +509,53 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           wave_lds_sync();
           int m = 0;
           const bool alt = sp.variant == 0;
-          if (Acc::LDS && depth == 1) {
-            // the common case: the leaf is a root child.  Simulation sim + i's
-            // select walks root -> leaf iff the root's PUCT picks the leaf's
-            // action, and then picks acts[i] there (its draw, by construction).
-            // The root's child stats are held in registers (the LDS mirror,
-            // updated with the same operations) and only its PUCT is re-run.
-            const int ac = sm.t.ract;
-            double P[G::AP], w[G::AP];
-            int n[G::AP], ch[G::AP];
-            uint64_t elig[G::AP], unexp = 0;
+          if (Acc::LDS && (depth == 1 || depth == 2)) {
+            // the common cases: the leaf is a root child or grandchild.
+            // Simulation sim + i's select walks root -> .. -> leaf iff every
+            // PUCT on the path keeps choosing the path's child, and then picks
+            // acts[i] at the leaf (its draw, by construction).  The path's
+            // levels are held in registers (PuctLevel) and only their PUCT
+            // checks are re-run.
+            PuctLevel<G> L0, L1;
+            uint64_t unexp = 0;
+            {
+              double P[G::AP], w[G::AP];
+              int n[G::AP], ch[G::AP];
+              uint64_t elig[G::AP];
 #pragma unroll
-            for (int j = 0; j < G::AP; ++j) {
-              const int a2 = lane + 64 * j;
-              const bool in = a2 < G::A;
-              P[j] = in ? T.root_prior(a2) : 0.0;
-              ch[j] = in ? T.child(0, a2) : -1;
-              n[j] = in ? sm.t.rvis[a2] : 0;
-              w[j] = in ? sm.t.rws[a2] : 0.0;
-              elig[j] = __ballot(P[j] > 0.0);
-              unexp |= __ballot(P[j] > 0.0 && ch[j] < 0);
+              for (int j = 0; j < G::AP; ++j) {
+                const int a2 = lane + 64 * j;
+                const bool in = a2 < G::A;
+                P[j] = in ? T.root_prior(a2) : 0.0;
+                ch[j] = in ? T.child(0, a2) : -1;
+                n[j] = in ? sm.t.rvis[a2] : 0;
+                w[j] = in ? sm.t.rws[a2] : 0.0;
+                elig[j] = __ballot(P[j] > 0.0);
+                unexp |= __ballot(P[j] > 0.0 && ch[j] < 0);
+              }
+              L0.init(P, n, w, elig, T.vis(0), sm.t.ract, true, sp);
+              if (depth == 2) {
+                const int p1 = T.path(1);
+#pragma unroll
+                for (int j = 0; j < G::AP; ++j) {
+                  const int a2 = lane + 64 * j;
+                  const bool in = a2 < G::A;
+                  P[j] = in ? (double)TV.prior[(size_t)p1 * G::A + a2] : 0.0;
+                  ch[j] = in ? TV.child[(size_t)p1 * G::A + a2] : -1;
+                  elig[j] = __ballot(P[j] > 0.0);
+                  unexp |= __ballot(P[j] > 0.0 && ch[j] < 0);
+                  n[j] = ch[j] >= 0 ? T.vis(ch[j]) : 0;
+                  w[j] = ch[j] >= 0 ? T.ws(ch[j]) : 0.0;
+                }
+                L1.init(P, n, w, elig, T.vis(p1), nact[leaf], false, sp);
+              }
             }
-            int nroot = T.vis(0);
             for (int i = 0; i < B; ++i) {
               const int ai = sm.u.f.acts[i];
               if (i > 0) {
-                bool ok = unexp == 0;                  // else select takes an unexpanded root child
-                if (ok) {
-                  int bc;
-                  ok = puct_pick<G>(P, n, w, elig, ch, nroot, true, sp, bc, &st) == ac;
-                }
+                // (an unexpanded child on the path's levels would be taken instead)
+                bool ok = unexp == 0 && L0.wins(sp);
+                if (ok && depth == 2) ok = L1.wins(sp);
                 if (!ok) {                             // the walk leaves the batch
                   st.lap(30);
                   const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, &st);
@@ -552,13 +569,12 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
               if (lane == (ai & 63)) T.set_child(leaf, ai, n2);
               const double v = sm.u.f.bv[i];
               st.lap(61);
-              backup<G>(T, 1, n2, v, alt);
+              backup<G>(T, depth, n2, v, alt);
               st.lap(62);
-              const double dvc = alt ? -v : v;         // the leaf's (depth 1) share
-#pragma unroll
-              for (int j = 0; j < G::AP; ++j)
-                if (lane == (ac & 63) && j == (ac >> 6)) { n[j] += 1; w[j] = w[j] + dvc; }
-              nroot += 1;
+              // the value shares of the path's depth-1 and depth-2 nodes
+              const double d1 = alt && (depth & 1) ? -v : v;          // depth 1 is depth + 1 - 1 steps above n2
+              L0.update(d1);
+              if (depth == 2) L1.update(alt ? -v : v);                 // the leaf (depth 2): one step above n2
               ++m;
             }
           } else {

@@ -572,6 +572,103 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
   return best_a;
 }
 
+// One level of a replayed select walk (speculative batches): node p whose
+// children are all expanded and whose PUCT (puct_pick) must keep choosing
+// the on-path child x.  Between replayed simulations only x's stats and p's
+// visit count change, so q of every other child, and the min / max of the
+// others' q, are kept; each check recomputes the u terms and compares every
+// score with x's.  Bit-identical to puct_pick: the same operations on the
+// same values (min / max are exact), the same first-maximum rule.  Wave-level.
+template <class G>
+struct PuctLevel {
+  double cP[G::AP], w[G::AP], q[G::AP], qn[G::AP];
+  int n[G::AP];
+  uint64_t elig[G::AP];
+  double lo_o, hi_o, lo, hi;    // min / max of q over eligible children other than x; over all
+  int N, x;
+
+  // P, nn, ww, el: p's child priors (f64; f32 values below the root), child
+  // visit counts, value sums and eligibility; nvis: p's visit count.
+  __device__ __forceinline__ void init(const double (&P)[G::AP], const int (&nn)[G::AP], const double (&ww)[G::AP],
+                                       const uint64_t (&el)[G::AP], int nvis, int xa, bool root,
+                                       const SearchParams& sp) {
+    const int lane = lane_id_local();
+    N = nvis;
+    x = xa;
+    lo_o = INFINITY;
+    hi_o = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      elig[j] = el[j];
+      n[j] = nn[j];
+      w[j] = ww[j];
+      // the first factor of u exactly as puct_pick forms it
+      cP[j] = root ? sp.c_puct * P[j] : (double)((float)sp.c_puct * (float)P[j]);
+      q[j] = 0.0;
+      if ((elig[j] >> lane) & 1ull) {
+        q[j] = n[j] > 0 ? w[j] / (double)n[j] : 0.0;
+        if (a != x) { lo_o = fmin(lo_o, q[j]); hi_o = fmax(hi_o, q[j]); }
+      }
+    }
+    wave_minmax(lo_o, hi_o);
+    renorm(true);
+  }
+  __device__ __forceinline__ double qx() const {
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (j == (x >> 6)) v = dpp::lane(q[j], x & 63);
+    return v;
+  }
+  // lo / hi with x's current q; qn of every child if they moved, else of x
+  __device__ __forceinline__ void renorm(bool all) {
+    const int lane = lane_id_local();
+    const double v = qx();
+    const double nlo = fmin(lo_o, v), nhi = fmax(hi_o, v);
+    all = all || nlo != lo || nhi != hi;
+    lo = nlo;
+    hi = nhi;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (all || (lane == (x & 63) && j == (x >> 6)))
+        qn[j] = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
+  }
+  // does p's PUCT pick x (self_play.py:290-308 / main.py:338-364)?
+  __device__ __forceinline__ bool wins(const SearchParams& sp) const {
+    const int lane = lane_id_local();
+    const double sq = sp.variant == 1 ? sqrt((double)(N + 1)) : sqrt((double)(N > 1 ? N : 1));
+    double sc[G::AP];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) sc[j] = qn[j] + (cP[j] * sq) / (double)(1 + n[j]);
+    double sx = 0.0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (j == (x >> 6)) sx = dpp::lane(sc[j], x & 63);
+    if (!(sx > -INFINITY)) return false;
+    uint64_t beat = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      beat |= __ballot(((elig[j] >> lane) & 1ull) && a != x && (sc[j] > sx || (sc[j] == sx && a < x)));
+    }
+    return beat == 0;
+  }
+  // after a backup: x visited once more with value share dv, p once more
+  __device__ __forceinline__ void update(double dv) {
+    const int lane = lane_id_local();
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (lane == (x & 63) && j == (x >> 6)) {
+        n[j] += 1;
+        w[j] = w[j] + dv;
+        q[j] = w[j] / (double)n[j];
+      }
+    N += 1;
+    renorm(false);
+  }
+};
+
 // ---------------------------------------------------------------------------
 // select_leaf (self_play.py:239-335).  Wave 0.  Returns the action to expand
 // at t.leaf, or -1 when the walk ends at a terminal node (t.leaf).  The path

@@ -105,6 +105,8 @@ def stamps_report():
                       "conv_slots_total": [round(float(allp[i]) * S) for i in (1, 6, 7, 20, 21, 29, 30)],
                       "slot3_total": round(float(allp[3]) * S),
                       "convs_per_search": float(buf[:, 59].astype(np.float64).mean() / 2),
+                      "top_slots_total": sorted([(int(i), round(float(allp[i]) * S)) for i in range(len(allp)) if allp[i] > 0],
+                                               key=lambda x: -x[1])[:24],
                       "implied_clock_GHz": total * S / (ms * 1e6)}))
 
 
