@@ -550,33 +550,53 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
                 L1.init(P, n, w, elig, T.vis(p1), nact[leaf], false, sp);
               }
             }
+            // The replayed simulations change only the registers; the tree
+            // takes their sums (same operations, same order) when the replay
+            // stops: before a select that leaves the batch, or at its end.
+            double wroot = T.ws(0);
+            auto writeback = [&](int cnt) {
+              if (lane == 0) {
+                T.set(0, L0.N, wroot);
+                const int p1 = T.path(1), n1 = L0.nx();
+                const double w1 = L0.wx();
+                T.set(p1, n1, w1);
+                sm.t.rvis[sm.t.ract] = n1;                 // the root-child mirror
+                sm.t.rws[sm.t.ract] = w1;
+                if (depth == 2) T.set(leaf, L1.nx(), L1.wx());
+              }
+              for (int i = lane; i < cnt; i += 64) {       // the new children
+                const int ai = sm.u.f.acts[i], n2 = nid + i;
+                T.set(n2, 1, 0.0 + sm.u.f.bv[i]);
+                nact[n2] = ai;
+                T.set_child(leaf, ai, n2);
+              }
+              wave_lds_sync();
+            };
             for (int i = 0; i < B; ++i) {
-              const int ai = sm.u.f.acts[i];
               if (i > 0) {
                 // (an unexpanded child on the path's levels would be taken instead)
                 bool ok = unexp == 0 && L0.wins(sp);
                 if (ok && depth == 2) ok = L1.wins(sp);
                 if (!ok) {                             // the walk leaves the batch
+                  writeback(m);
+                  m = -m - 1;                          // (written back)
                   st.lap(30);
                   const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, &st);
                   if (lane == 0) sm.t.action = a2;
                   break;
                 }
               }
-              const int n2 = nid + i;
               st.lap(60);
-              if (lane == 0) { T.init(n2); nact[n2] = ai; }
-              if (lane == (ai & 63)) T.set_child(leaf, ai, n2);
+              // backpropagate(path + [child], v): node at depth d gets v * (-1)^(depth + 1 - d)
               const double v = sm.u.f.bv[i];
-              st.lap(61);
-              backup<G>(T, depth, n2, v, alt);
+              wroot = wroot + (alt && ((depth + 1) & 1) ? -v : v);   // root: depth + 1 steps above
+              L0.update(alt && (depth & 1) ? -v : v);  // depth 1: depth steps above the new child
+              if (depth == 2) L1.update(alt ? -v : v); // the leaf: one step above
               st.lap(62);
-              // the value shares of the path's depth-1 and depth-2 nodes
-              const double d1 = alt && (depth & 1) ? -v : v;          // depth 1 is depth + 1 - 1 steps above n2
-              L0.update(d1);
-              if (depth == 2) L1.update(alt ? -v : v);                 // the leaf (depth 2): one step above n2
               ++m;
             }
+            if (m >= 0) writeback(m);
+            else m = -m - 1;
           } else {
             for (int i = 0; i < B; ++i) {
               const int ai = sm.u.f.acts[i];

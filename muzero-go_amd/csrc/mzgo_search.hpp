@@ -101,6 +101,9 @@ struct TreeAcc {
   __device__ __forceinline__ void init(int n) {
     if constexpr (L) { t.svis[n] = 0; t.sws[n] = 0.0; } else { T.visits[n] = 0; T.wsum[n] = 0.0; }
   }
+  __device__ __forceinline__ void set(int n, int vis, double ws) {
+    if constexpr (L) { t.svis[n] = vis; t.sws[n] = ws; } else { T.visits[n] = vis; T.wsum[n] = ws; }
+  }
   __device__ __forceinline__ int path(int i) const { if constexpr (L) return t.spath[i]; else return T.path[i]; }
   __device__ __forceinline__ void set_path(int i, int n) { if constexpr (L) t.spath[i] = n; else T.path[i] = n; }
   __device__ __forceinline__ int child(int n, int a) const {
@@ -653,6 +656,21 @@ struct PuctLevel {
       beat |= __ballot(((elig[j] >> lane) & 1ull) && a != x && (sc[j] > sx || (sc[j] == sx && a < x)));
     }
     return beat == 0;
+  }
+  // x's visit count and value sum (every lane)
+  __device__ __forceinline__ int nx() const {
+    int v = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (j == (x >> 6)) v = __builtin_amdgcn_readlane(n[j], x & 63);
+    return v;
+  }
+  __device__ __forceinline__ double wx() const {
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (j == (x >> 6)) v = dpp::lane(w[j], x & 63);
+    return v;
   }
   // after a backup: x visited once more with value share dv, p once more
   __device__ __forceinline__ void update(double dv) {
