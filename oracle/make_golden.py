@@ -21,6 +21,9 @@ Fixtures:
                        oracle.goenv.GoEnv, (a) with counter-stream hooks and
                        (b) with the reference's own seeded RNGs
   mctsmain_*.npz       main.py's MCTS.run (main.py:246-368) under the same hooks
+  train_5x5_c32.npz    main.py's MuZeroAgent.train (main.py:381-522), two
+                       batches on synthetic trajectories with fixed start
+                       indices: losses, priorities, lr, final weights
 Usage:  python -m oracle.make_golden   (from the repo root)
 """
 import json
@@ -235,6 +238,84 @@ def make_mcts_main(mn, name, N, S, n_moves, seed=13, game=4, move=6, C=96):
     print("mcts(main.py)", name, "root N", root.visit_count, "value", root.value(), "depth", depth)
 
 
+def synthetic_trajectories(N, B, seed):
+    """main.py-format trajectories (main.py:636-713) from random legal
+    playouts on the oracle GoEnv rules: observations T+2, actions T,
+    policies T (random distributions), rewards T+1 (0 per move, a winner)."""
+    from oracle import gogame
+    A = N * N + 1
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(B):
+        T = int(rng.integers(4, 16))
+        st = gogame.init_state(N)
+        obs, acts, pols, rews = [st.copy()], [], [], []
+        for _t in range(T):
+            legal = np.flatnonzero(gogame.invalid_moves(st) == 0)
+            a = int(rng.choice(legal)) if rng.random() > 0.1 else N * N
+            st = gogame.next_state(st, a)
+            p = rng.random(A)
+            acts.append(a)
+            pols.append(p / p.sum())
+            rews.append(0.0)
+            obs.append(st.copy())
+            if gogame.game_ended(st):
+                break
+        rews.append(float(rng.choice([-1.0, 1.0])))
+        obs.append(st.copy())
+        out.append(dict(observations=obs, actions=acts, rewards=rews, policies=pols))
+    return out
+
+
+def pack_trajectories(trajs):
+    lens = np.array([len(t["actions"]) for t in trajs], dtype=np.int64)
+    return dict(traj_len=lens,
+                traj_obs=np.concatenate([np.stack(t["observations"]) for t in trajs]),
+                traj_actions=np.concatenate([np.array(t["actions"], dtype=np.int64) for t in trajs]),
+                traj_rewards=np.concatenate([np.array(t["rewards"], dtype=np.float64) for t in trajs]),
+                traj_policies=np.concatenate([np.stack(t["policies"]) for t in trajs]))
+
+
+def make_train(mn, N=5, C=32, B=4, seed=5, batches=2):
+    """main.py's MuZeroAgent.train (main.py:381-522) on synthetic
+    trajectories: random.randint (the start index, :395) replaced by a fixed
+    sequence, the replay buffer by a stub that returns the whole batch.
+    Records the returned losses, the priorities handed back, the lr and the
+    weights after ``batches`` steps."""
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    mn.config.board_size = N
+    mn.config.max_action_size = A
+    mn.config.latent_dim = C
+    trajs = synthetic_trajectories(N, B, seed)
+    rng = np.random.default_rng(seed + 1)
+    starts = [int(rng.integers(0, len(t["actions"]))) for _ in range(batches) for t in trajs]
+    agent = mn.MuZeroAgent(N, C, A, 4)
+    agent.net.load_state_dict({k: torch.from_numpy(v) for k, v in deterministic_state_dict(C, A, seed).items()})
+    it = iter(starts)
+    prios = []
+
+    class Buf:
+        def sample(self, bs):
+            return trajs, list(range(bs))
+
+        def update_priorities(self, idx, p):
+            prios.append(list(p))
+
+    saved = mn.random.randint
+    mn.random.randint = lambda lo, hi: next(it)
+    try:
+        losses = [agent.train(Buf(), B) for _ in range(batches)]
+    finally:
+        mn.random.randint = saved
+    sd = {f"w_{k}": v.detach().numpy().astype(np.float32) for k, v in agent.net.state_dict().items()}
+    np.savez_compressed(os.path.join(GOLDEN, f"train_{N}x{N}_c{C}.npz"), N=np.int64(N), C=np.int64(C),
+                        B=np.int64(B), seed=np.int64(seed), starts=np.array(starts, dtype=np.int64),
+                        losses=np.array(losses, dtype=np.float64), priorities=np.array(prios, dtype=np.float64),
+                        lr=np.float64(agent.optimizer.param_groups[0]["lr"]), **pack_trajectories(trajs), **sd)
+    print("train", N, C, "losses", losses)
+
+
 def _pack_record(rec):
     types = {
         "rewards": [type(r).__name__ for r in rec["rewards"]],
@@ -316,6 +397,17 @@ def main():
     make_mcts_main(mn, "5x5_s25_mid", 5, 25, 7)
     make_mcts_main(mn, "9x9_s200_empty", 9, 200, 0)
     make_mcts_main(mn, "9x9_s200_mid", 9, 200, 26)
+    make_train(mn)
+
+
+def train_only():
+    """Regenerate only the trainer fixture (``python -m oracle.make_golden train``)."""
+    os.makedirs(GOLDEN, exist_ok=True)
+    sys.path.insert(0, REPO)
+    import_reference()
+    torch.set_num_threads(1)
+    import main as mn  # noqa: E402
+    make_train(mn)
 
 
 def main_only():
@@ -331,4 +423,4 @@ def main_only():
 
 
 if __name__ == "__main__":
-    main_only() if sys.argv[1:] == ["main"] else main()
+    {"main": main_only, "train": train_only}.get(sys.argv[1] if sys.argv[1:] else "", main)()

@@ -1,0 +1,105 @@
+"""Trainer ingestion on the GPU (mzgo.trainer).
+
+* main.py's training step (reference mode) on the GPU vs the step recorded
+  from the reference (tests/golden/train_5x5_c32.npz), to GPU-conv tolerance;
+* main.py-format trajectories from the device self-play (MainSelfPlay, main.py's
+  6x6 / latent_dim 128 configuration): lengths, legal replay on the oracle
+  board (bit-exact planes), policies, winners;
+* batched mode: its bootstrap values come from one HIP initial_inference
+  launch and must equal the torch forward's; with B = 1 it is the reference
+  step.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_trainer import _Buf, _unpack, run_reference_step
+
+pytestmark = pytest.mark.gpu
+
+
+def test_reference_step_on_gpu_matches_main_py(golden_dir):
+    g = np.load(f"{golden_dir}/train_5x5_c32.npz")
+    net, tr, buf, losses = run_reference_step(g, device="cuda")
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-4)
+    np.testing.assert_allclose(np.array(buf.prios), g["priorities"], rtol=1e-4)
+    sd = net.state_dict()
+    for k in sd:
+        np.testing.assert_allclose(sd[k].detach().cpu().numpy(), g["w_" + k], rtol=1e-3, atol=2e-5, err_msg=k)
+
+
+def test_main_selfplay_trajectories_replay_on_the_oracle_board():
+    import mzgo
+    from mzgo.trainer import MainSelfPlay
+    from oracle import gogame
+    N, C, G, S = 6, 128, 8, 32                     # main.py's Config (main.py:27-53)
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda().eval()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 3))
+    trajs = MainSelfPlay(net, G, S, seed=21).play()
+    assert len(trajs) == G
+    for t in trajs:
+        T = len(t["actions"])
+        assert 1 <= T <= int(1.5 * N * N)
+        assert len(t["observations"]) == T + 2 and len(t["rewards"]) == T + 1 and len(t["policies"]) == T
+        st = gogame.init_state(N)
+        for k in range(T):
+            np.testing.assert_array_equal(t["observations"][k], st)
+            p = t["policies"][k]
+            assert p.shape == (A,) and abs(p.sum() - 1.0) < 1e-9
+            st = gogame.next_state(st, t["actions"][k])
+        np.testing.assert_array_equal(t["observations"][T], st)
+        np.testing.assert_array_equal(t["observations"][T + 1], st)
+        ended = gogame.game_ended(st)
+        winner = float(gogame.winning(st)) if ended else 0.0
+        assert t["rewards"][-1] == winner
+        if not ended:
+            assert T == int(1.5 * N * N) and t["rewards"][-2] == -0.5
+
+
+def test_batched_bootstrap_on_hip_equals_torch():
+    import mzgo
+    from mzgo.trainer import MuZeroTrainer, initial_inference_torch
+    from oracle.make_golden import synthetic_trajectories
+    N, C = 5, 96
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 4))
+    trajs = synthetic_trajectories(N, 6, seed=9)
+    obs = torch.as_tensor(np.stack([o for t in trajs for o in t["observations"]]), dtype=torch.float32).cuda()
+    with torch.no_grad():
+        _, v_hip, _ = net.initial_inference(obs)
+        _, v_t, _ = initial_inference_torch(net, obs)
+    np.testing.assert_allclose(v_hip.cpu().numpy(), v_t.cpu().numpy(), rtol=0, atol=1e-5)
+    # B = 1: one optimizer step on one trajectory either way
+    res = {}
+    for mode in ("reference", "batched"):
+        net2 = mzgo.MuZeroNet(C, A).cuda()
+        net2.load_state_dict(mzgo.deterministic_state_dict(C, A, 4))
+        tr = MuZeroTrainer(net2, mode=mode, start_index=lambda T: 0)
+        res[mode] = (tr.train(_Buf(trajs[:1]), 1), net2.state_dict())
+    assert res["batched"][0] == pytest.approx(res["reference"][0], rel=1e-4)
+    for k in res["reference"][1]:
+        np.testing.assert_allclose(res["batched"][1][k].cpu().numpy(), res["reference"][1][k].cpu().numpy(),
+                                   rtol=1e-3, atol=1e-5, err_msg=k)
+
+
+def test_batched_mode_trains_on_selfplay_output():
+    import mzgo
+    from mzgo.trainer import MainSelfPlay, MultiVersionReplayBuffer, MuZeroTrainer
+    N, C, G, S = 6, 128, 8, 16
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 5))
+    buf = MultiVersionReplayBuffer(100)
+    for t in MainSelfPlay(net, G, S, seed=3).play():
+        buf.add(t)
+    np.random.seed(0)
+    tr = MuZeroTrainer(net, mode="batched")
+    before = {k: v.clone() for k, v in net.state_dict().items()}
+    loss = tr.train(buf, 4)
+    assert np.isfinite(loss)
+    assert any(not torch.equal(before[k], v) for k, v in net.state_dict().items())
+    # the engine picks up the new weights for the next self-play round
+    trajs = MainSelfPlay(net, 2, S, seed=4).play()
+    assert len(trajs) == 2
