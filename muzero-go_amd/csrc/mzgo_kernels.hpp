@@ -394,6 +394,166 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
   }
 }
 
+// Parallel replay of a speculative batch (factored dynamics, LDS trees).
+//
+// The batch's B children of `leaf` (depth D, path p_0 = root .. p_D = leaf)
+// stand for simulations sim .. sim + B - 1; simulation sim + i (i >= 1)
+// reaches the leaf again iff, at every level l < D, p_l's PUCT still picks
+// the path child x_l = p_(l+1) after the i earlier simulations were backed
+// up (it then takes acts[i] at the leaf: its draw, by construction).  Those
+// i backups are known in advance (their values are the batch's), so every
+// check (i, l) is independent: the state it sees is p_l's children as they
+// are now, except x_l with n_x + i visits and value sum W_x(i) (the prefix
+// sum, in simulation order, of its shares), and p_l with N + i visits.  All
+// (i, l) checks run at once over the workgroup with puct_pick's operations
+// and first-maximum rule; the batch is accepted up to the first failing i,
+// and the tree takes the accepted simulations' sums.  Returns the number of
+// accepted simulations m >= 1 (all threads; synchronised).
+template <class G, int DMAX>
+struct VerifyLds {
+  double cP[DMAX][64 * G::AP];      // c_puct * P as puct_pick forms it
+  double q[DMAX][64 * G::AP];       // W / N of every child, now
+  int n[DMAX][64 * G::AP];
+  uint64_t elig[DMAX][G::AP];
+  double lo_o[DMAX], hi_o[DMAX];    // min / max of q over eligible children other than x
+  int x[DMAX], n0[DMAX], N0[DMAX];
+  double wpre[DMAX][G::A + 1];      // x_l's value sum after i accepted simulations
+  double wroot[G::A + 1];           // the root's value sum after i
+  int fail;
+};
+constexpr int kVerifyDepth = 12;
+
+template <class G, class Acc>
+__device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, Acc& T,
+                                            int* nact, int leaf, int D, int B, int nid) {
+  if constexpr (!decltype(sm.u.f)::BATCH) {
+    return 0;                                       // (no speculative batches without the batch LDS)
+  } else {
+  typedef VerifyLds<G, kVerifyDepth> V;
+  static_assert(sizeof(V) <= sizeof(sm.u.f.wv), "verification arrays overlay the batch buffers");
+  V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+  const int lane = lane_id_local();
+  const bool alt = sp.variant == 0;
+  const double* bv = sm.u.f.bv;
+  // share of the node at depth d in a batch child's backup: v (-1)^(D + 1 - d)
+  auto share = [&](int d, double v) { return alt && ((D + 1 - d) & 1) ? -v : v; };
+  if (threadIdx.x == 0) vl.fail = B;
+  // ---- 1. the levels (one wave each) and the root's own sums ----
+  for (int l = wave; l <= D; l += G::WAVES) {
+    if (l == D) {                                   // the root's value sum after i simulations
+      if (lane == 0) {
+        double w = T.ws(0);
+        vl.wroot[0] = w;
+        for (int k = 0; k < B - 1; ++k) { w = w + share(0, bv[k]); vl.wroot[k + 1] = w; }
+        vl.wroot[B] = w + share(0, bv[B - 1]);
+      }
+      continue;
+    }
+    const int p = T.path(l);
+    const int xa = l == 0 ? sm.t.ract : nact[T.path(l + 1)];
+    double lo = INFINITY, hi = -INFINITY, wx = 0.0;
+    int nx = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      const bool in = a < G::A;
+      double P, w = 0.0;
+      int n = 0;
+      if (l == 0) {
+        P = in ? T.root_prior(a) : 0.0;
+        if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }
+      } else {
+        P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
+        const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
+        if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+      }
+      const bool e = P > 0.0;
+      const uint64_t el = __ballot(e);
+      const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
+      vl.cP[l][a] = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
+      vl.q[l][a] = q;
+      vl.n[l][a] = n;
+      if (lane == 0) vl.elig[l][j] = el;
+      if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
+      if (j == (xa >> 6)) { wx = dpp::lane(w, xa & 63); nx = __builtin_amdgcn_readlane(n, xa & 63); }
+    }
+    wave_minmax(lo, hi);
+    if (lane == 0) {
+      vl.lo_o[l] = lo;
+      vl.hi_o[l] = hi;
+      vl.x[l] = xa;
+      vl.n0[l] = nx;
+      vl.N0[l] = T.vis(p);
+      double w = wx;                                // x_l = p_(l+1): depth l + 1
+      vl.wpre[l][0] = w;
+      for (int k = 0; k < B; ++k) { w = w + share(l + 1, bv[k]); vl.wpre[l][k + 1] = w; }
+    }
+  }
+  __syncthreads();
+  // ---- 2. every (i, l) check at once ----
+  const int items = (B - 1) * D;
+  for (int it = wave; it < items; it += G::WAVES) {
+    const int i = 1 + it / D, l = it - (i - 1) * D;
+    if (__hip_atomic_load(&vl.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) continue;
+    const int xa = vl.x[l];
+    const int nx = vl.n0[l] + i, N = vl.N0[l] + i;
+    const double qx = nx > 0 ? vl.wpre[l][i] / (double)nx : 0.0;
+    const double lo = fmin(vl.lo_o[l], qx), hi = fmax(vl.hi_o[l], qx);
+    const double sq = sp.variant == 1 ? sqrt((double)(N + 1)) : sqrt((double)(N > 1 ? N : 1));
+    double sc[G::AP];
+    bool el[G::AP];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      el[j] = (vl.elig[l][j] >> lane) & 1ull;
+      const bool isx = a == xa;
+      const double q = isx ? qx : vl.q[l][a];
+      const int n = isx ? nx : vl.n[l][a];
+      const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
+      sc[j] = qn + (vl.cP[l][a] * sq) / (double)(1 + n);
+    }
+    double sx = 0.0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (j == (xa >> 6)) sx = dpp::lane(sc[j], xa & 63);
+    uint64_t beat = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      beat |= __ballot(el[j] && a != xa && (sc[j] > sx || (sc[j] == sx && a < xa)));
+    }
+    if ((beat != 0 || !(sx > -INFINITY)) && lane == 0) atomicMin(&vl.fail, i);
+  }
+  __syncthreads();
+  const int m = vl.fail;
+  // ---- 3. the tree takes the m accepted simulations ----
+  if (wave_id() == 0) {
+    if (lane <= D) {                                // path nodes p_0 .. p_D
+      if (lane == 0) {
+        T.set(0, T.vis(0) + m, vl.wroot[m]);
+      } else {
+        const int l = lane - 1;                     // p_lane = x_l
+        T.set(T.path(lane), vl.n0[l] + m, vl.wpre[l][m]);
+        if (lane == 1) { sm.t.rvis[sm.t.ract] = vl.n0[0] + m; sm.t.rws[sm.t.ract] = vl.wpre[0][m]; }
+      }
+    }
+    wave_lds_sync();
+    for (int i = lane; i < m; i += 64) {            // the new children
+      const int ai = sm.u.f.acts[i], n2 = nid + i;
+      const double v = 0.0 + bv[i];
+      T.set(n2, 1, v);
+      nact[n2] = ai;
+      T.set_child(leaf, ai, n2);
+      if (leaf == 0) T.add_root_child(ai, v);       // (set_child zeroed the mirror)
+    }
+    if (lane == 0) { sm.t.newest = -1; sm.t.ycache = leaf; }
+  }
+  __syncthreads();
+  return m;
+  }
+}
+
 // The simulations of one search with the tree accessor Acc (LDS or HBM stats).
 //
 // Factored dynamics also batch SPECULATIVELY: once a simulation's select ends
@@ -503,101 +663,21 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         batch_expand<G>(sm, np, sp, TV, B, nid, &st);
         __syncthreads();
         st.lap(5);
+        if (Acc::LDS && depth <= kVerifyDepth) {
+          const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid);
+          nodes += m;
+          sim += m;
+          st.lap(63);
+          if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
+          continue;
+        }
         if (wave_id() == 0) {
           const int lane = lane_id_local();
           if (lane == 0) { sm.t.newest = -1; sm.t.ycache = leaf; }
           wave_lds_sync();
           int m = 0;
           const bool alt = sp.variant == 0;
-          if (Acc::LDS && (depth == 1 || depth == 2)) {
-            // the common cases: the leaf is a root child or grandchild.
-            // Simulation sim + i's select walks root -> .. -> leaf iff every
-            // PUCT on the path keeps choosing the path's child, and then picks
-            // acts[i] at the leaf (its draw, by construction).  The path's
-            // levels are held in registers (PuctLevel) and only their PUCT
-            // checks are re-run.
-            PuctLevel<G> L0, L1;
-            uint64_t unexp = 0;
-            {
-              double P[G::AP], w[G::AP];
-              int n[G::AP], ch[G::AP];
-              uint64_t elig[G::AP];
-#pragma unroll
-              for (int j = 0; j < G::AP; ++j) {
-                const int a2 = lane + 64 * j;
-                const bool in = a2 < G::A;
-                P[j] = in ? T.root_prior(a2) : 0.0;
-                ch[j] = in ? T.child(0, a2) : -1;
-                n[j] = in ? sm.t.rvis[a2] : 0;
-                w[j] = in ? sm.t.rws[a2] : 0.0;
-                elig[j] = __ballot(P[j] > 0.0);
-                unexp |= __ballot(P[j] > 0.0 && ch[j] < 0);
-              }
-              L0.init(P, n, w, elig, T.vis(0), sm.t.ract, true, sp);
-              if (depth == 2) {
-                const int p1 = T.path(1);
-#pragma unroll
-                for (int j = 0; j < G::AP; ++j) {
-                  const int a2 = lane + 64 * j;
-                  const bool in = a2 < G::A;
-                  P[j] = in ? (double)TV.prior[(size_t)p1 * G::A + a2] : 0.0;
-                  ch[j] = in ? TV.child[(size_t)p1 * G::A + a2] : -1;
-                  elig[j] = __ballot(P[j] > 0.0);
-                  unexp |= __ballot(P[j] > 0.0 && ch[j] < 0);
-                  n[j] = ch[j] >= 0 ? T.vis(ch[j]) : 0;
-                  w[j] = ch[j] >= 0 ? T.ws(ch[j]) : 0.0;
-                }
-                L1.init(P, n, w, elig, T.vis(p1), nact[leaf], false, sp);
-              }
-            }
-            // The replayed simulations change only the registers; the tree
-            // takes their sums (same operations, same order) when the replay
-            // stops: before a select that leaves the batch, or at its end.
-            double wroot = T.ws(0);
-            auto writeback = [&](int cnt) {
-              if (lane == 0) {
-                T.set(0, L0.N, wroot);
-                const int p1 = T.path(1), n1 = L0.nx();
-                const double w1 = L0.wx();
-                T.set(p1, n1, w1);
-                sm.t.rvis[sm.t.ract] = n1;                 // the root-child mirror
-                sm.t.rws[sm.t.ract] = w1;
-                if (depth == 2) T.set(leaf, L1.nx(), L1.wx());
-              }
-              for (int i = lane; i < cnt; i += 64) {       // the new children
-                const int ai = sm.u.f.acts[i], n2 = nid + i;
-                T.set(n2, 1, 0.0 + sm.u.f.bv[i]);
-                nact[n2] = ai;
-                T.set_child(leaf, ai, n2);
-              }
-              wave_lds_sync();
-            };
-            for (int i = 0; i < B; ++i) {
-              if (i > 0) {
-                // (an unexpanded child on the path's levels would be taken instead)
-                bool ok = unexp == 0 && L0.wins(sp);
-                if (ok && depth == 2) ok = L1.wins(sp);
-                if (!ok) {                             // the walk leaves the batch
-                  writeback(m);
-                  m = -m - 1;                          // (written back)
-                  st.lap(30);
-                  const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, &st);
-                  if (lane == 0) sm.t.action = a2;
-                  break;
-                }
-              }
-              st.lap(60);
-              // backpropagate(path + [child], v): node at depth d gets v * (-1)^(depth + 1 - d)
-              const double v = sm.u.f.bv[i];
-              wroot = wroot + (alt && ((depth + 1) & 1) ? -v : v);   // root: depth + 1 steps above
-              L0.update(alt && (depth & 1) ? -v : v);  // depth 1: depth steps above the new child
-              if (depth == 2) L1.update(alt ? -v : v); // the leaf: one step above
-              st.lap(62);
-              ++m;
-            }
-            if (m >= 0) writeback(m);
-            else m = -m - 1;
-          } else {
+          {
             for (int i = 0; i < B; ++i) {
               const int ai = sm.u.f.acts[i];
               if (i > 0) {

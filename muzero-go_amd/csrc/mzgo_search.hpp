@@ -13,6 +13,7 @@
 // and scores float64, backup value float64 = reward + 0.99 * value.
 #pragma once
 #include "mzgo_common.hpp"
+#include <type_traits>
 
 namespace mzgo {
 
@@ -582,60 +583,82 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
 // others' q, are kept; each check recomputes the u terms and compares every
 // score with x's.  Bit-identical to puct_pick: the same operations on the
 // same values (min / max are exact), the same first-maximum rule.  Wave-level.
-template <class G>
+// Per-lane arrays of a PuctLevel, kept in LDS (a = lane + 64 j): the replay
+// loop runs on a register file the rest of the kernel has filled, and LDS
+// reads are far cheaper than the scratch reloads the spills would cost.
+template <class G, class CP>
+struct PuctMem {
+  CP cP[G::AP][64];
+  double q[G::AP][64], qn[G::AP][64];
+  int n[G::AP][64];
+};
+
+template <class G, bool ROOT>
 struct PuctLevel {
-  double cP[G::AP], w[G::AP], q[G::AP], qn[G::AP];
-  int n[G::AP];
+  // the first factor of u exactly as puct_pick forms it: root priors f64
+  // (c_puct * P in f64); below the root an f32 product (exact in f32)
+  typedef typename std::conditional<ROOT, double, float>::type cp_t;
+  typedef PuctMem<G, cp_t> Mem;
+  Mem& m;
   uint64_t elig[G::AP];
   double lo_o, hi_o, lo, hi;    // min / max of q over eligible children other than x; over all
-  int N, x;
+  double w_x;                   // x's value sum (the other children's sums stay fixed)
+  int n_x, N, x;
+
+  __device__ __forceinline__ explicit PuctLevel(Mem& mem) : m(mem) {}
 
   // P, nn, ww, el: p's child priors (f64; f32 values below the root), child
   // visit counts, value sums and eligibility; nvis: p's visit count.
   __device__ __forceinline__ void init(const double (&P)[G::AP], const int (&nn)[G::AP], const double (&ww)[G::AP],
-                                       const uint64_t (&el)[G::AP], int nvis, int xa, bool root,
-                                       const SearchParams& sp) {
+                                       const uint64_t (&el)[G::AP], int nvis, int xa, const SearchParams& sp) {
     const int lane = lane_id_local();
     N = nvis;
     x = xa;
     lo_o = INFINITY;
     hi_o = -INFINITY;
+    w_x = 0.0;
+    n_x = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
       const int a = lane + 64 * j;
       elig[j] = el[j];
-      n[j] = nn[j];
-      w[j] = ww[j];
-      // the first factor of u exactly as puct_pick forms it
-      cP[j] = root ? sp.c_puct * P[j] : (double)((float)sp.c_puct * (float)P[j]);
-      q[j] = 0.0;
+      m.n[j][lane] = nn[j];
+      if constexpr (ROOT) m.cP[j][lane] = sp.c_puct * P[j];
+      else m.cP[j][lane] = (float)sp.c_puct * (float)P[j];
+      double q = 0.0;
       if ((elig[j] >> lane) & 1ull) {
-        q[j] = n[j] > 0 ? w[j] / (double)n[j] : 0.0;
-        if (a != x) { lo_o = fmin(lo_o, q[j]); hi_o = fmax(hi_o, q[j]); }
+        q = nn[j] > 0 ? ww[j] / (double)nn[j] : 0.0;
+        if (a != x) { lo_o = fmin(lo_o, q); hi_o = fmax(hi_o, q); }
       }
+      m.q[j][lane] = q;
+      if (j == (x >> 6)) { w_x = dpp::lane(ww[j], x & 63); n_x = __builtin_amdgcn_readlane(nn[j], x & 63); }
     }
     wave_minmax(lo_o, hi_o);
+    lo = NAN;
     renorm(true);
   }
-  __device__ __forceinline__ double qx() const {
-    double v = 0.0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (j == (x >> 6)) v = dpp::lane(q[j], x & 63);
-    return v;
-  }
+  __device__ __forceinline__ double qx() const { return n_x > 0 ? w_x / (double)n_x : 0.0; }
   // lo / hi with x's current q; qn of every child if they moved, else of x
   __device__ __forceinline__ void renorm(bool all) {
     const int lane = lane_id_local();
     const double v = qx();
     const double nlo = fmin(lo_o, v), nhi = fmax(hi_o, v);
-    all = all || nlo != lo || nhi != hi;
+    all = all || !(nlo == lo) || !(nhi == hi);
     lo = nlo;
     hi = nhi;
+    if (all) {
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (all || (lane == (x & 63) && j == (x >> 6)))
-        qn[j] = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
+      for (int j = 0; j < G::AP; ++j) {
+        double q = m.q[j][lane];
+        if (lane == (x & 63) && j == (x >> 6)) { q = v; m.q[j][lane] = v; }
+        m.qn[j][lane] = hi > lo ? (q - lo) / (hi - lo) : q;
+      }
+    } else if (lane == (x & 63)) {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j)
+        if (j == (x >> 6)) { m.q[j][lane] = v; m.qn[j][lane] = hi > lo ? (v - lo) / (hi - lo) : v; }
+    }
+    wave_lds_sync();
   }
   // does p's PUCT pick x (self_play.py:290-308 / main.py:338-364)?
   __device__ __forceinline__ bool wins(const SearchParams& sp) const {
@@ -643,7 +666,8 @@ struct PuctLevel {
     const double sq = sp.variant == 1 ? sqrt((double)(N + 1)) : sqrt((double)(N > 1 ? N : 1));
     double sc[G::AP];
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j) sc[j] = qn[j] + (cP[j] * sq) / (double)(1 + n[j]);
+    for (int j = 0; j < G::AP; ++j)
+      sc[j] = m.qn[j][lane] + ((double)m.cP[j][lane] * sq) / (double)(1 + m.n[j][lane]);
     double sx = 0.0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j)
@@ -657,31 +681,18 @@ struct PuctLevel {
     }
     return beat == 0;
   }
-  // x's visit count and value sum (every lane)
-  __device__ __forceinline__ int nx() const {
-    int v = 0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (j == (x >> 6)) v = __builtin_amdgcn_readlane(n[j], x & 63);
-    return v;
-  }
-  __device__ __forceinline__ double wx() const {
-    double v = 0.0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (j == (x >> 6)) v = dpp::lane(w[j], x & 63);
-    return v;
-  }
+  __device__ __forceinline__ int nx() const { return n_x; }
+  __device__ __forceinline__ double wx() const { return w_x; }
   // after a backup: x visited once more with value share dv, p once more
   __device__ __forceinline__ void update(double dv) {
     const int lane = lane_id_local();
+    n_x += 1;
+    w_x = w_x + dv;
+    if (lane == (x & 63)) {
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (lane == (x & 63) && j == (x >> 6)) {
-        n[j] += 1;
-        w[j] = w[j] + dv;
-        q[j] = w[j] / (double)n[j];
-      }
+      for (int j = 0; j < G::AP; ++j)
+        if (j == (x >> 6)) m.n[j][lane] = n_x;
+    }
     N += 1;
     renorm(false);
   }
