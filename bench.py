@@ -224,23 +224,34 @@ def main():
         mfma_exec = mfma_launch / avg_kern_s / 1e12
         peak_mfma = 157.3
         bytes_sim = algorithmic_bytes(N, C, G)
-        gbps = per_launch_sims * bytes_sim / avg_kern_s / 1e9
+        gbps_8d = per_launch_sims * bytes_sim / avg_kern_s / 1e9
         peak_hbm = 8000.0
         if args.dynamics == "factored":
-            # one 3x3 conv per new PARENT (a few per search) instead of one per
-            # simulation: the MFMA roofline of the reference formulation no longer
-            # binds (equiv_direct_conv_tflops exceeds the fp32 MFMA peak); the
-            # remaining per-simulation work is latency-bound tree + elementwise
-            # traffic, reported against HBM with §8(d)'s bytes per simulation
+            # The factored algorithm's own HBM bytes: per simulation the child's
+            # E[a] row (9 C f32) and its prior and child-id rows (2 A x 4 B); per
+            # parent conv the rebuilt latent (written, read) and its Y (written,
+            # read into LDS); per move the representation's input and latent and
+            # the record.  (SURVEY §8(d)'s direct-formulation bytes and FLOPs per
+            # simulation are reported beside it: the factored kernel runs past
+            # both of those rooflines because it no longer does that work.)
+            CS = (N * N + 15) // 16 * 16
+            launch_convs = convs / args.steps
+            fact_bytes = (per_launch_sims * (9 * C * 4 + 2 * A * 4)
+                          + launch_convs * (2 * C * CS * 4 + 2 * N * N * C * 4)
+                          + per_launch_moves * ((6 * N * N + 2 * C * CS) * 4 + 2 * N * N + A * 8 + 32))
+            gbps = fact_bytes / avg_kern_s / 1e9
             roof = {"bound": "hbm", "kernel": "k_selfplay_move", "achieved": gbps, "peak": peak_hbm,
                     "unit": "GB/s", "frac": gbps / peak_hbm, "traffic": None,
-                    "algorithmic_bytes_per_sim": bytes_sim, "sims_per_launch": per_launch_sims,
+                    "algorithmic_bytes_per_launch": fact_bytes, "sims_per_launch": per_launch_sims,
                     "avg_launch_ms": avg_kern_s * 1e3,
+                    "survey_8d_bytes_per_sim": bytes_sim, "equiv_survey_8d_gbps": gbps_8d,
                     "equiv_direct_conv_tflops": equiv_tflops,
                     "equiv_direct_conv_frac_of_fp32_mfma": equiv_tflops / peak_mfma,
                     "dynamics_convs_per_move": convs / max(1.0, moves / world),
                     "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak_mfma,
-                    "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a]))"}
+                    "note": "latency/LDS-bound (per-game serial chain on one CU); see DESIGN.md section 5",
+                    "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a])), "
+                                 "batched + replayed expansions"}
         else:
             roof = {"bound": "mfma", "kernel": "k_selfplay_move", "achieved": equiv_tflops,
                     "peak": peak_mfma, "unit": "TFLOP/s", "frac": equiv_tflops / peak_mfma, "traffic": None,
