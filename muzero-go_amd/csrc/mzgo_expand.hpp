@@ -169,67 +169,101 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
   }
 }
 
-// One child's heads by ONE wave (the batched root phase): xw [3][CS] gets
-// the reward / value / policy sums of relu(Y + E[a]) per cell, Y [CELLS][C]
-// and E[a] [9][C] and the head weights hw [3][C] all in LDS.  Lane (j, cg):
-// channel float4s c4 = j + 8k, cells 8 pass + cg.  Wave-level; the caller
+// Per-lane plan of a wave's expansion passes (expand_wave): lane (j, cg)
+// takes cells cg + 8 p in pass p; off packs, per pass, the byte offset of
+// the cell's region row E[a][region] (two 16-bit halves per dword; cells past
+// the board read region 0 and are discarded).  Built once per batch.
+template <class G>
+struct ExpandPlan {
+  static constexpr int PASSES = (G::CELLS + 7) / 8;
+  uint32_t off[(PASSES + 1) / 2];
+  static_assert(8 * PASSES <= G::CS, "the last pass's cells stay inside the head rows");
+  static_assert(8 * 4 * G::C < 65536, "16-bit region offsets");
+  __device__ __forceinline__ void init() {
+    const int cg = lane_id_local() >> 3;
+#pragma unroll
+    for (int i = 0; i < (PASSES + 1) / 2; ++i) off[i] = 0;
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int cell = cg + 8 * p;
+      const uint32_t reg = cell < G::CELLS ? (uint32_t)region_of<G>(cell) : 0u;
+      off[p >> 1] |= (reg * (uint32_t)G::C * 4u) << (16 * (p & 1));
+    }
+  }
+  __device__ __forceinline__ uint32_t at(int p) const { return (off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu; }
+};
+
+// One child's heads by ONE wave (batch_expand), Y [CELLS][C], E[a] [9][C]
+// and the head weights hw [3][C] (reward, value, policy) all in LDS:
+//   * the policy 1x1-conv sum of relu(Y + E[a]) per cell -> xw[2][cell];
+//   * the reward and value heads only enter the network through their means
+//     over the cells (self_play.py:91-94, :105-110), and a 1x1 conv is
+//     linear, so their totals are taken channel-first:
+//         sum_cells sum_c w_c relu(v)  =  sum_c w_c S_c,  S_c = sum_cells relu(v)
+//     -> rsum, vsum (no biases; every lane).  One packed add per channel pair
+//     and cell instead of two FMAs and two per-cell reductions.
+// Lane (j, cg): channel float4s c4 = j + 8k, cells cg + 8p (every pass
+// unrolled: Y at immediate offsets, E through the plan's offsets).  The 8
+// lanes of a cell end with its full policy sum and all write it (same value,
+// same address), so no lane is masked off; the last pass's cells past the
+// board land in the row padding and stay out of S.  Wave-level; the caller
 // orders xw for the wave's readers (wave_lds_sync).
 template <class G>
-__device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw) {
+__device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw,
+                                            const ExpandPlan<G>& plan, float& rsum, float& vsum) {
   typedef ExpandShape<G> X;
+  constexpr int P = ExpandPlan<G>::PASSES;
   const int lane = lane_id_local();
   const int j = lane & 7, cg = lane >> 3;
-  const f32x4* Y4 = reinterpret_cast<const f32x4*>(yc);
-  const f32x4* E4 = reinterpret_cast<const f32x4*>(ew);
   const f32x4* W4 = reinterpret_cast<const f32x4*>(hw);
-  f32x4 wr[X::PERL], wv[X::PERL], wp[X::PERL];
+  f32x4 wp[X::PERL];
+  f32x2 s2[X::PERL][2];
 #pragma unroll
   for (int k = 0; k < X::PERL; ++k) {
-    const int c4 = j + 8 * k;
-    wr[k] = W4[c4]; wv[k] = W4[X::C4 + c4]; wp[k] = W4[2 * X::C4 + c4];
+    wp[k] = W4[2 * X::C4 + j + 8 * k];
+    s2[k][0] = f32x2{0.f, 0.f};
+    s2[k][1] = f32x2{0.f, 0.f};
   }
-  constexpr int U = 2;                        // passes per iteration: loads of both issued first
-  for (int p0 = 0; p0 < G::CELLS; p0 += 8 * U) {
-    f32x4 y[U][X::PERL], e[U][X::PERL];
-    int cell[U];
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(yc) + cg * X::C4 + j;   // + pass * 8 * C4 + 8 k
+  const char* Eb = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew) + j);
+  float* xr = xw + 2 * G::CS + cg;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      cell[u] = p0 + 8 * u + cg;
-      const int cl = cell[u] < G::CELLS ? cell[u] : G::CELLS - 1;
-      const int reg = region_of<G>(cl);
+  for (int p = 0; p < P; ++p) {
+    const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + plan.at(p));
+    f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
-      for (int k = 0; k < X::PERL; ++k) {
-        y[u][k] = Y4[cl * X::C4 + j + 8 * k];
-        e[u][k] = E4[reg * X::C4 + j + 8 * k];
+    for (int k = 0; k < X::PERL; ++k) {
+      y[k] = Y4[p * 8 * X::C4 + 8 * k];
+      e[k] = E4[8 * k];
+    }
+    const bool live = G::CELLS % 8 == 0 || p < P - 1 || cg + 8 * p < G::CELLS;
+    f32x2 hp2 = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) {
+#pragma unroll
+      for (int q = 0; q < 4; q += 2) {
+        f32x2 v = f32x2{y[k][q], y[k][q + 1]} + f32x2{e[k][q], e[k][q + 1]};
+        v.x = v.x > 0.f ? v.x : 0.f;
+        v.y = v.y > 0.f ? v.y : 0.f;
+        hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
+        if (!live) v = f32x2{0.f, 0.f};
+        s2[k][q >> 1] = s2[k][q >> 1] + v;
       }
     }
+    xr[8 * p] = sum8(hp2.x + hp2.y);
+  }
+  f32x2 dr2 = {0.f, 0.f}, dv2 = {0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      // channel pairs in packed f32 (v_pk_add / v_pk_fma: two channels per
-      // instruction), two partial sums per head
-      f32x2 hr2 = {0.f, 0.f}, hv2 = {0.f, 0.f}, hp2 = {0.f, 0.f};
+  for (int k = 0; k < X::PERL; ++k) {
+    const f32x4 wr = W4[j + 8 * k], wv = W4[X::C4 + j + 8 * k];
 #pragma unroll
-      for (int k = 0; k < X::PERL; ++k) {
-#pragma unroll
-        for (int q = 0; q < 4; q += 2) {
-          f32x2 v = f32x2{y[u][k][q], y[u][k][q + 1]} + f32x2{e[u][k][q], e[u][k][q + 1]};
-          v.x = v.x > 0.f ? v.x : 0.f;
-          v.y = v.y > 0.f ? v.y : 0.f;
-          hr2 = __builtin_elementwise_fma(f32x2{wr[k][q], wr[k][q + 1]}, v, hr2);
-          hv2 = __builtin_elementwise_fma(f32x2{wv[k][q], wv[k][q + 1]}, v, hv2);
-          hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
-        }
-      }
-      float hr = sum8(hr2.x + hr2.y);
-      float hv = sum8(hv2.x + hv2.y);
-      float hp = sum8(hp2.x + hp2.y);
-      if (j == 0 && cell[u] < G::CELLS) {
-        xw[cell[u]] = hr;
-        xw[G::CS + cell[u]] = hv;
-        xw[2 * G::CS + cell[u]] = hp;
-      }
+    for (int q = 0; q < 4; q += 2) {
+      dr2 = __builtin_elementwise_fma(f32x2{wr[q], wr[q + 1]}, s2[k][q >> 1], dr2);
+      dv2 = __builtin_elementwise_fma(f32x2{wv[q], wv[q + 1]}, s2[k][q >> 1], dv2);
     }
   }
+  rsum = wave_sum(dr2.x + dr2.y);
+  vsum = wave_sum(dv2.x + dv2.y);
 }
 
 // The latent of a node that is about to become a parent: relu(Y_par + E[a])

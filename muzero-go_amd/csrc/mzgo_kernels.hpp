@@ -273,28 +273,31 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
     const int lane = lane_id_local();
     if (wave == 0) return;
     auto& W = L.wv[wave];
+    ExpandPlan<G> plan;
+    plan.init();
     for (int k = wave - 1; k < B; k += G::WAVES - 1) {
       while (__hip_atomic_load(&sm.t.npick, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
         __builtin_amdgcn_s_sleep(2);
+      unsigned long long t0 = st ? st->now() : 0, t1;
       const int a = L.acts[k], nid = nid0 + k;
       const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
-      if (st) st->lap(64);
       for (int i = lane; i < 9 * G::C / 4; i += 64) reinterpret_cast<f32x4*>(W.ew)[i] = e4[i];
       wave_lds_sync();
-      if (st) st->lap(65);
-      expand_wave<G>(W.xw, L.yc, W.ew, L.hw);
+      if (st) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
+      float rsum, vsum;
+      expand_wave<G>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
       wave_lds_sync();
-      if (st) st->lap(66);
+      if (st) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
       float r, v, x[G::AP];
-      heads_value<G, 1>(W.xw, true, sm.t.hsc, r, v);
+      heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
       logits_regs<G, 1>(W.xw, true, sm.t.hsc, x);
       int* crow = TV.child + (size_t)nid * G::A;
       for (int i = lane; i < G::A; i += 64) crow[i] = -1;
-      if (st) st->lap(67);
+      if (st) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
       child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
       if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
       wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
-      if (st) st->lap(68);
+      if (st) { t1 = st->now(); st->wave_add(67, t1 - t0); st->wave_add(68, 1); }
     }
   }
 }
@@ -323,7 +326,7 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
 template <class G, class Acc>
 __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                           const TreeView& TV, Acc& T, float* pool, float* scratch, int* nact,
-                                          uint64_t key) {
+                                          uint64_t key, Stamp* st = nullptr) {
   auto& L = sm.u.f;
   if constexpr (!decltype(sm.u.f)::BATCH) {
     return 0;
@@ -348,9 +351,11 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
                                         nullptr);
     __syncthreads();
+    if (st) st->lap(60);
     load_y<G>(sm, pool, np.head_w);
     if (threadIdx.x == 0) sm.t.npick = 0;
     __syncthreads();
+    if (st) st->lap(61);
     if (wave_id() == 0) {
       // the simulations' choices: sim k takes the r_k-th (ascending) of the
       // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
@@ -365,8 +370,9 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       }
       pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick);
     }
-    batch_expand<G>(sm, np, sp, TV, K, 1);
+    batch_expand<G>(sm, np, sp, TV, K, 1, st);
     __syncthreads();
+    if (st) st->lap(62);
     if (wave_id() == 0) {
       const int lane = lane_id_local();
       // the K backups of backpropagate(path + [child], v) (self_play.py:337-343)
@@ -588,7 +594,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   Stamp st(E.stamps);
   int sim = 0;
   if (factored) {
-    sim = root_batch<G, Acc>(sm, np, sp, TV, T, pool, scratch, nact, key);
+    sim = root_batch<G, Acc>(sm, np, sp, TV, T, pool, scratch, nact, key, &st);
     nodes += sim;
     convs += sim > 0 ? 1 : 0;
     st.lap(4);

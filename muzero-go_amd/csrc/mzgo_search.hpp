@@ -266,6 +266,26 @@ __device__ __forceinline__ void heads_value(const float* hp, bool has_reward, co
   }
 }
 
+// value and reward heads (self_play.py:91-94, :105-110) from the totals over
+// cells and channels of their 1x1 convs without biases (expand_wave):
+// mean = total / CELLS + bias.  Every lane.
+template <class G>
+__device__ __forceinline__ void heads_from_totals(float rsum, float vsum, const float* hsc, float& reward,
+                                                  float& value) {
+  const float vmean = vsum / (float)G::CELLS + hsc[HS_VB];
+  value = vmean * hsc[HS_VFCW] + hsc[HS_VFCB];
+  const float rmean = rsum / (float)G::CELLS + hsc[HS_RB];
+  const int lane = lane_id_local();
+  float h = 0.f;
+  if (lane < 16) {
+    h = rmean * hsc[HS_FC1W + lane] + hsc[HS_FC1B + lane];
+    h = h > 0.f ? h : 0.f;
+    h = h * hsc[HS_FC2W + lane];
+  }
+  h = wave_sum(h);
+  reward = h + hsc[HS_FC2B];
+}
+
 // policy logits of a lane's actions a = lane + 64 j (cells, then the learned
 // pass logit), in registers.  One wave.
 template <class G, int NPART>

@@ -96,12 +96,14 @@ def stamps_report():
                       "wave_stage_wait": [round(float(v)) for v in allp[44:56]],
                       "factored_expand_pre_barrier": round(float(allp[56])),
                       "wave1_logits": round(float(allp[57])), "wave1_priors": round(float(allp[58])),
-                      "replay_select_to_accept": round(float(allp[60])), "replay_init_setchild": round(float(allp[61])),
-                      "replay_backup": round(float(allp[62])),
+                      "root_conv_loady_expand_total": [round(float(allp[i]) * S) for i in (60, 61, 62)],
+                      "expand_per_child_copyE_heads_logits_priors": [round(float(allp[i] / max(allp[68], 1e-9)))
+                                                                     for i in (64, 65, 66, 67)],
+                      "expanded_children_per_search": float(allp[68] * S),
                       "batch_end_barrier_total": round(float(allp[63]) * 2 * S / 2),
                       "batches_per_search": float(buf[:, 31].astype(np.float64).mean() / 2),
                       "batched_sims_per_search": float(buf[:, 28].astype(np.float64).mean() / 2),
-                      "batch_detail_total_w0": [round(float(v) * S) for v in allp[64:72]],
+                      "batch_detail_total_w0": [round(float(v) * S) for v in allp[69:72]],
                       "conv_slots_total": [round(float(allp[i]) * S) for i in (1, 6, 7, 20, 21, 29, 30)],
                       "slot3_total": round(float(allp[3]) * S),
                       "convs_per_search": float(buf[:, 59].astype(np.float64).mean() / 2),
