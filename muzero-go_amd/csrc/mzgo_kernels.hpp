@@ -264,7 +264,7 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
 // r + discount * v.  Waves 1.. take the children; wave 0 publishes the
 // actions meanwhile (pick_sequence, sm.t.npick) and returns at once.  All
 // threads; the caller synchronises.
-template <class G>
+template <class G, bool LAZY>
 __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                              const TreeView& TV, int B, int nid0, Stamp* st = nullptr) {
   auto& L = sm.u.f;
@@ -294,7 +294,17 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
       int* crow = TV.child + (size_t)nid * G::A;
       for (int i = lane; i < G::A; i += 64) crow[i] = -1;
       if (st) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
-      child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
+      if constexpr (LAZY) {
+        // the row keeps the logits until a select first reaches the child
+        // (select_leaf -> settle_priors); most children never are
+        float* prow = TV.prior + (size_t)nid * G::A;
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j)
+          if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
+        if (lane == 0) atomicOr(&sm.t.rawp[nid >> 5], 1u << (nid & 31));
+      } else {
+        child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
+      }
       if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
       wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
       if (st) { t1 = st->now(); st->wave_add(67, t1 - t0); st->wave_add(68, 1); }
@@ -370,7 +380,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       }
       pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick);
     }
-    batch_expand<G>(sm, np, sp, TV, K, 1, st);
+    batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, st);
     __syncthreads();
     if (st) st->lap(62);
     if (wave_id() == 0) {
@@ -666,7 +676,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick);
           st.lap(71);
         }
-        batch_expand<G>(sm, np, sp, TV, B, nid, &st);
+        batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, &st);
         __syncthreads();
         st.lap(5);
         if (Acc::LDS && depth <= kVerifyDepth) {
@@ -808,6 +818,24 @@ __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int
   }
 }
 
+// Turn every prior row still holding logits into priors (TreeLds::rawp):
+// the search API exports whole trees (mzgo_tree_export), self-play does not
+// and skips this.  All threads; the batch buffers serve as per-wave scratch.
+template <class G>
+__device__ __forceinline__ void settle_all_priors(Smem<G>& sm, const TreeView& TV, int nodes, int variant) {
+  if constexpr (decltype(sm.u.f)::BATCH && G::TREE_CAP > 0) {
+    const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+    auto& W = sm.u.f.wv[wave];
+    const int lim = nodes < G::TREE_CAP ? nodes : G::TREE_CAP;
+    for (int n = 1 + wave; n < lim; n += G::WAVES) {
+      if (!sm.t.is_raw(n)) continue;
+      float q[G::AP];
+      settle_priors<G>(sm.t, TV.prior + (size_t)n * G::A, n, variant, W.fb, W.db, q);
+    }
+  }
+  __syncthreads();
+}
+
 template <int N, int C>
 __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_search(NetParams np, SearchParams sp, EngineArrays E,
                                                       const float* __restrict__ root_obs,
@@ -821,6 +849,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const uint64_t key = stream_key(sp.seed, (uint32_t)(game_base + g), (uint32_t)move_index);
   run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return o[c * G::CELLS + j]; },
                 noise ? noise + (size_t)g * G::A : nullptr, key);
+  settle_all_priors<G>(sm, TreeViewOf<G>::make(E, g), E.nodes[g], sp.variant);
   search_outputs<G>(E, g, out_visits, out_value);
 }
 

@@ -79,6 +79,14 @@ struct TreeLds {
   float newp[G::A];
   int newest;              // id of the newest node (-1: none)
   int newp_node;           // node whose priors newp holds (atomic, workgroup scope)
+  // nodes whose prior row still holds the policy LOGITS (batched expansions
+  // of LDS trees: a row is turned into priors when a select first reaches the
+  // node -- most children never are; see batch_expand)
+  uint32_t rawp[G::TREE_CAP > 0 ? (G::TREE_CAP + 31) / 32 : 1];
+  __device__ __forceinline__ bool is_raw(int n) const {
+    if constexpr (G::TREE_CAP > 0) return n < G::TREE_CAP && ((rawp[n >> 5] >> (n & 31)) & 1u);
+    else return false;
+  }
 };
 
 // Tree accessor: node stats, path and the root's child row / priors either in
@@ -327,17 +335,14 @@ __device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward,
 // wave.  One wave; values stay in registers except for the ordered sum.
 // fbuf / dbuf: this wave's LDS scratch for the ordered sums (A entries each).
 template <class G>
-__device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::AP], float* __restrict__ dst,
-                                             int node = -1, int variant = 0, float* fbuf = nullptr,
-                                             double* dbuf = nullptr) {
+__device__ __forceinline__ void child_prior_regs(const TreeLds<G>& t, const float (&x)[G::AP], float (&q)[G::AP],
+                                                 int variant, float* fbuf, double* dbuf) {
   const int lane = lane_id_local();
-  if (!fbuf) { fbuf = t.fbuf; dbuf = t.dbuf; }
   float p[G::AP];
   double m[G::AP];
   softmax_regs<G>(x, p);
 #pragma unroll
   for (int j = 0; j < G::AP; ++j) m[j] = lane + 64 * j < G::A ? mask_of<G>(t, lane + 64 * j) : 0.0;
-  float q[G::AP];
   if (variant == 1) {
     // main.py:299-309: softmax[a] where valid_mask[a] > 0, not renormalised
 #pragma unroll
@@ -364,6 +369,16 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::
       for (int j = 0; j < G::AP; ++j) q[j] = (float)(m[j] / ms);
     }
   }
+}
+
+template <class G>
+__device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::AP], float* __restrict__ dst,
+                                             int node = -1, int variant = 0, float* fbuf = nullptr,
+                                             double* dbuf = nullptr) {
+  const int lane = lane_id_local();
+  if (!fbuf) { fbuf = t.fbuf; dbuf = t.dbuf; }
+  float q[G::AP];
+  child_prior_regs<G>(t, x, q, variant, fbuf, dbuf);
 #pragma unroll
   for (int j = 0; j < G::AP; ++j) {
     const int a = lane + 64 * j;
@@ -375,6 +390,22 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::
   // publish newp for a select running concurrently on another wave
   if (node >= 0 && lane == 0)
     __hip_atomic_store(&t.newp_node, node, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// A raw prior row (policy logits, see TreeLds::rawp) -> the node's child
+// priors, in place; q gets them too.  One wave; fbuf / dbuf: its LDS scratch.
+template <class G>
+__device__ __forceinline__ void settle_priors(TreeLds<G>& t, float* row, int node, int variant, float* fbuf,
+                                              double* dbuf, float (&q)[G::AP]) {
+  const int lane = lane_id_local();
+  float x[G::AP];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) x[j] = lane + 64 * j < G::A ? row[lane + 64 * j] : 0.f;
+  child_prior_regs<G>(t, x, q, variant, fbuf, dbuf);
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j)
+    if (lane + 64 * j < G::A) row[lane + 64 * j] = q[j];
+  if (lane == 0) atomicAnd(&t.rawp[node >> 5], ~(1u << (node & 31)));
 }
 
 // Gamma(alpha) by Marsaglia-Tsang with the alpha+1 boost, from the counter
@@ -768,6 +799,19 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         P[j] = a < G::A ? (double)t.rowc_prior[a] : 0.0;
         ch[j] = a < G::A ? t.rowc_child[a] : -1;
       }
+    } else if (t.is_raw(node)) {               // first arrival: the row holds logits
+      // t.fbuf / t.dbuf are wave 1's while it forms the newest node's priors
+      if (t.newest >= 0)
+        while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
+          __builtin_amdgcn_s_sleep(1);
+      float q[G::AP];
+      settle_priors<G>(t, const_cast<float*>(pr_row), node, sp.variant, t.fbuf, t.dbuf, q);
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        P[j] = a < G::A ? (double)q[j] : 0.0;
+        ch[j] = a < G::A ? T.T.child[(size_t)node * G::A + a] : -1;
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) {
@@ -873,6 +917,8 @@ __device__ __forceinline__ void backup(Acc& T, int depth, int nid, double v, boo
 template <class G, class Acc>
 __device__ __forceinline__ void tree_reset_root(Acc& T) {
   for (int a = threadIdx.x; a < G::A; a += G::THREADS) T.set_child(0, a, -1);
+  if constexpr (G::TREE_CAP > 0)
+    for (int i = threadIdx.x; i < (G::TREE_CAP + 31) / 32; i += G::THREADS) T.t.rawp[i] = 0u;
   if (threadIdx.x == 0) { T.init(0); T.set_path(0, 0); }
 }
 
