@@ -62,7 +62,7 @@ struct ExpandLds {
     float fb[64 * G::AP];                 // ordered-sum scratch (child_priors)
     double db[64 * G::AP];
   };
-  Wave wv[BATCH ? G::WAVES : 1];          // (after the batch: the replay's PuctLevel arrays)
+  Wave wv[BATCH ? G::WAVES : 1];          // (after the batch: verify_batch's arrays)
   double bv[BATCH ? G::A : 1];            // backup value of each batched child
   int acts[BATCH ? G::A : 1];             // action of each batched child
 };

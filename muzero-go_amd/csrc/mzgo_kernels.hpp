@@ -260,10 +260,11 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
 // Batch expansion (factored dynamics): children i < B of one parent whose Y
 // is in L.yc (and the head weights in L.hw), child i = node nid0 + i via
 // action L.acts[i]; one wave per child: E[a] into LDS, heads, the child's
-// prior row (child_priors) and child row, L.bv[i] = its backup value
-// r + discount * v.  Waves 1.. take the children; wave 0 publishes the
-// actions meanwhile (pick_sequence, sm.t.npick) and returns at once.  All
-// threads; the caller synchronises.
+// prior row (LAZY: its logits, see TreeLds::rawp) and child row, L.bv[i] =
+// its backup value r + discount * v.  Each wave claims the next child
+// (sm.t.ngrab, reset with sm.t.npick by the caller) and waits until
+// sm.t.npick > k (wave 0 publishes the actions, pick_sequence, before it
+// joins).  All threads; the caller synchronises.
 template <class G, bool LAZY>
 __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                              const TreeView& TV, int B, int nid0, Stamp* st = nullptr) {
@@ -271,22 +272,50 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
   if constexpr (decltype(sm.u.f)::BATCH) {
     const int wave = __builtin_amdgcn_readfirstlane(wave_id());
     const int lane = lane_id_local();
-    if (wave == 0) return;
     auto& W = L.wv[wave];
     ExpandPlan<G> plan;
     plan.init();
-    for (int k = wave - 1; k < B; k += G::WAVES - 1) {
+    // E[a] of the wave's next child, loaded into registers while the current
+    // child's heads and rows are written (its action is published by then
+    // unless the picks are late; the copy then reads E at the top)
+    constexpr int E4N = 9 * G::C / 4, EP = (E4N + 63) / 64;
+    f32x4 epre[EP];
+    int epre_a = -1;
+    f32x4* ewl = reinterpret_cast<f32x4*>(W.ew);
+    // children are claimed one at a time (wave 0 joins late, after the picks)
+    auto grab = [&]() {
+      int v = 0;
+      if (lane == 0) v = atomicAdd(&sm.t.ngrab, 1);
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+    for (int k = grab(), kn; k < B; k = kn) {
       while (__hip_atomic_load(&sm.t.npick, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= k)
         __builtin_amdgcn_s_sleep(2);
       unsigned long long t0 = st ? st->now() : 0, t1;
-      const int a = L.acts[k], nid = nid0 + k;
-      const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
-      for (int i = lane; i < 9 * G::C / 4; i += 64) reinterpret_cast<f32x4*>(W.ew)[i] = e4[i];
+      const int a = __builtin_amdgcn_readfirstlane(L.acts[k]), nid = nid0 + k;
+      if (a == epre_a) {
+#pragma unroll
+        for (int e = 0; e < EP; ++e)
+          if (lane + 64 * e < E4N) ewl[lane + 64 * e] = epre[e];
+      } else {
+        const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
+        for (int i = lane; i < E4N; i += 64) ewl[i] = e4[i];
+      }
       wave_lds_sync();
       if (st) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
       float rsum, vsum;
       expand_wave<G>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
       wave_lds_sync();
+      epre_a = -1;
+      kn = grab();
+      {
+        if (kn < B && __hip_atomic_load(&sm.t.npick, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > kn) {
+          epre_a = __builtin_amdgcn_readfirstlane(L.acts[kn]);
+          const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)epre_a * 9 * G::C);
+#pragma unroll
+          for (int e = 0; e < EP; ++e) epre[e] = e4[lane + 64 * e < E4N ? lane + 64 * e : 0];
+        }
+      }
       if (st) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
       float r, v, x[G::AP];
       heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
@@ -363,7 +392,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     __syncthreads();
     if (st) st->lap(60);
     load_y<G>(sm, pool, np.head_w);
-    if (threadIdx.x == 0) sm.t.npick = 0;
+    if (threadIdx.x == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
     __syncthreads();
     if (st) st->lap(61);
     if (wave_id() == 0) {
@@ -378,7 +407,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         el[j] = __ballot(a < G::A && T.root_prior(a) > 0.0);
         n += __popcll(el[j]);
       }
-      pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick);
+      pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
     }
     batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, st);
     __syncthreads();
@@ -663,7 +692,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
             if (threadIdx.x == 0) sm.t.rowc_node = leaf;
           }
         }
-        if (threadIdx.x == 0) { sm.u.f.acts[0] = a; sm.t.npick = 1; }
+        if (threadIdx.x == 0) { sm.u.f.acts[0] = a; sm.t.npick = 1; sm.t.ngrab = 0; }
         __syncthreads();
         st.lap(70);
         if (wave_id() == 0) {
@@ -673,7 +702,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
 #pragma unroll
           for (int j = 0; j < G::AP; ++j)
             if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
-          pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick);
+          pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1);
           st.lap(71);
         }
         batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, &st);

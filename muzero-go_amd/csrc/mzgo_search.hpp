@@ -53,6 +53,7 @@ struct TreeLds {
   int leaf, action, nid, depth, nodes, bcast;
   int yready;              // select's leaf already has a child (its conv Y exists: factored mode)
   int npick;               // batch actions published so far (pick_sequence -> batch_expand)
+  int ngrab;               // batch children claimed by the expanding waves so far
   int nunexp;              // select's leaf: number of unexpanded eligible children
   uint64_t umask[G::AP];   //   and their bitmask (a = 64 j + bit), the chosen one included
   int ycache;              // node whose Y the LDS copy holds (factored mode), -1: none
@@ -518,53 +519,66 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 
 // The choices of simulations sim0, sim0 + 1, ... (count of them) that each
 // take an unexpanded eligible child of the same node: simulation sim0 + i
-// picks the r-th (ascending) of the n - i still unexpanded ones (bitmask m),
-// r = randbelow(draw(key, TAG_SELECT, sim0 + i), n - i) -- select_leaf's
-// random.choice (self_play.py:283-287) replayed.  out[i0 + i] (LDS) gets
-// the action, and *progress (LDS, if given) the number published so far.
-// Wave-level (wave-uniform results); m is updated.
+// picks the r_i-th (ascending) of the n - i still unexpanded ones (bitmask m),
+// r_i = randbelow(draw(key, TAG_SELECT, sim0 + i), n - i) -- select_leaf's
+// random.choice (self_play.py:283-287) replayed.  The draws are made in
+// parallel (lane i = lane + 64 q); then, pick by pick, every element keeps
+// its rank among the remaining ones (lane a = lane + 64 q), the pick is the
+// remaining element of rank r_i (a ballot), and the ranks above it drop by
+// one.  out[i0 + i] (LDS) gets the actions; *progress (LDS, if given) is
+// published after the first `head` picks and every 12 after.  Wave-level.
 template <class G>
-__device__ __forceinline__ void pick_sequence(uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
-                                              int sim0, int* out, int* progress = nullptr) {
+__device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
+                                              int sim0, int* out, int* progress = nullptr, int head = 1) {
   const int lane = lane_id_local();
-  uint32_t rr[G::AP];
+  uint32_t r[G::AP];
 #pragma unroll
-  for (int q = 0; q < G::AP; ++q) {              // the draws in parallel, lane i = lane + 64 q
+  for (int q = 0; q < G::AP; ++q) {
     const int i = lane + 64 * q;
-    rr[q] = i < count ? randbelow(draw(key, TAG_SELECT, (uint64_t)(sim0 + i)), (uint32_t)(n - i)) : 0u;
+    r[q] = i < count ? randbelow(draw(key, TAG_SELECT, (uint64_t)(sim0 + i)), (uint32_t)(n - i)) : 0u;
   }
-  // the masks as scalars (wave-uniform): the serial picks run on the SALU
-  uint64_t ms[G::AP];
+  uint64_t rem[G::AP];
 #pragma unroll
   for (int j = 0; j < G::AP; ++j) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m[j]);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m[j] >> 32));
-    ms[j] = ((uint64_t)hi << 32) | lo;
+    rem[j] = ((uint64_t)hi << 32) | lo;
   }
-  for (int i = 0; i < count; ++i) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int q = 0; q < G::AP; ++q)
-      if ((i >> 6) == q) r = (uint32_t)__builtin_amdgcn_readlane((int)rr[q], i & 63);
-    int best = -1;
+  uint32_t rank[G::AP];
+  {
+    uint32_t below = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const uint32_t c = __popcll(ms[j]);
-      if (best < 0 && r < c) best = 64 * j + kth_set_bit(ms[j], r);
-      else if (best < 0) r -= c;
-    }
-    if (best < 0) best = 0;                      // unreachable: r < n - i = popcount(m)
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if ((best >> 6) == j) ms[j] &= ~(1ull << (best & 63));
-    if (lane == 0) {
-      out[i0 + i] = best;
-      // published as soon as made: batch_expand's waves start on their children
-      if (progress) __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      rank[j] = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(rem[j] >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)rem[j], 0u));
+      below += (uint32_t)__popcll(rem[j]);
     }
   }
+  int next_pub = head < count ? head : count;
+  for (int i = 0; i < count; ++i) {
+    uint32_t ri = 0;
 #pragma unroll
-  for (int j = 0; j < G::AP; ++j) m[j] = ms[j];
+    for (int q = 0; q < G::AP; ++q)
+      if ((i >> 6) == q) ri = (uint32_t)__builtin_amdgcn_readlane((int)r[q], i & 63);
+    int a = 0;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const uint64_t hit = __ballot(rank[j] == ri) & rem[j];
+      if (!found && hit) { a = 64 * j + __ffsll((long long)hit) - 1; found = true; }
+    }
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      if ((a >> 6) == j) rem[j] &= ~(1ull << (a & 63));
+      rank[j] -= (lane + 64 * j > a) ? 1u : 0u;
+    }
+    if (lane == 0) out[i0 + i] = a;
+    if (progress && i + 1 == next_pub) {
+      wave_lds_sync();
+      if (lane == 0) __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      next_pub = next_pub + 12 < count ? next_pub + 12 : count;
+    }
+  }
 }
 
 // PUCT over the eligible, all expanded children elig (self_play.py:290-308;
@@ -626,128 +640,6 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
   }
   return best_a;
 }
-
-// One level of a replayed select walk (speculative batches): node p whose
-// children are all expanded and whose PUCT (puct_pick) must keep choosing
-// the on-path child x.  Between replayed simulations only x's stats and p's
-// visit count change, so q of every other child, and the min / max of the
-// others' q, are kept; each check recomputes the u terms and compares every
-// score with x's.  Bit-identical to puct_pick: the same operations on the
-// same values (min / max are exact), the same first-maximum rule.  Wave-level.
-// Per-lane arrays of a PuctLevel, kept in LDS (a = lane + 64 j): the replay
-// loop runs on a register file the rest of the kernel has filled, and LDS
-// reads are far cheaper than the scratch reloads the spills would cost.
-template <class G, class CP>
-struct PuctMem {
-  CP cP[G::AP][64];
-  double q[G::AP][64], qn[G::AP][64];
-  int n[G::AP][64];
-};
-
-template <class G, bool ROOT>
-struct PuctLevel {
-  // the first factor of u exactly as puct_pick forms it: root priors f64
-  // (c_puct * P in f64); below the root an f32 product (exact in f32)
-  typedef typename std::conditional<ROOT, double, float>::type cp_t;
-  typedef PuctMem<G, cp_t> Mem;
-  Mem& m;
-  uint64_t elig[G::AP];
-  double lo_o, hi_o, lo, hi;    // min / max of q over eligible children other than x; over all
-  double w_x;                   // x's value sum (the other children's sums stay fixed)
-  int n_x, N, x;
-
-  __device__ __forceinline__ explicit PuctLevel(Mem& mem) : m(mem) {}
-
-  // P, nn, ww, el: p's child priors (f64; f32 values below the root), child
-  // visit counts, value sums and eligibility; nvis: p's visit count.
-  __device__ __forceinline__ void init(const double (&P)[G::AP], const int (&nn)[G::AP], const double (&ww)[G::AP],
-                                       const uint64_t (&el)[G::AP], int nvis, int xa, const SearchParams& sp) {
-    const int lane = lane_id_local();
-    N = nvis;
-    x = xa;
-    lo_o = INFINITY;
-    hi_o = -INFINITY;
-    w_x = 0.0;
-    n_x = 0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      elig[j] = el[j];
-      m.n[j][lane] = nn[j];
-      if constexpr (ROOT) m.cP[j][lane] = sp.c_puct * P[j];
-      else m.cP[j][lane] = (float)sp.c_puct * (float)P[j];
-      double q = 0.0;
-      if ((elig[j] >> lane) & 1ull) {
-        q = nn[j] > 0 ? ww[j] / (double)nn[j] : 0.0;
-        if (a != x) { lo_o = fmin(lo_o, q); hi_o = fmax(hi_o, q); }
-      }
-      m.q[j][lane] = q;
-      if (j == (x >> 6)) { w_x = dpp::lane(ww[j], x & 63); n_x = __builtin_amdgcn_readlane(nn[j], x & 63); }
-    }
-    wave_minmax(lo_o, hi_o);
-    lo = NAN;
-    renorm(true);
-  }
-  __device__ __forceinline__ double qx() const { return n_x > 0 ? w_x / (double)n_x : 0.0; }
-  // lo / hi with x's current q; qn of every child if they moved, else of x
-  __device__ __forceinline__ void renorm(bool all) {
-    const int lane = lane_id_local();
-    const double v = qx();
-    const double nlo = fmin(lo_o, v), nhi = fmax(hi_o, v);
-    all = all || !(nlo == lo) || !(nhi == hi);
-    lo = nlo;
-    hi = nhi;
-    if (all) {
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        double q = m.q[j][lane];
-        if (lane == (x & 63) && j == (x >> 6)) { q = v; m.q[j][lane] = v; }
-        m.qn[j][lane] = hi > lo ? (q - lo) / (hi - lo) : q;
-      }
-    } else if (lane == (x & 63)) {
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j)
-        if (j == (x >> 6)) { m.q[j][lane] = v; m.qn[j][lane] = hi > lo ? (v - lo) / (hi - lo) : v; }
-    }
-    wave_lds_sync();
-  }
-  // does p's PUCT pick x (self_play.py:290-308 / main.py:338-364)?
-  __device__ __forceinline__ bool wins(const SearchParams& sp) const {
-    const int lane = lane_id_local();
-    const double sq = sp.variant == 1 ? sqrt((double)(N + 1)) : sqrt((double)(N > 1 ? N : 1));
-    double sc[G::AP];
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      sc[j] = m.qn[j][lane] + ((double)m.cP[j][lane] * sq) / (double)(1 + m.n[j][lane]);
-    double sx = 0.0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (j == (x >> 6)) sx = dpp::lane(sc[j], x & 63);
-    if (!(sx > -INFINITY)) return false;
-    uint64_t beat = 0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      beat |= __ballot(((elig[j] >> lane) & 1ull) && a != x && (sc[j] > sx || (sc[j] == sx && a < x)));
-    }
-    return beat == 0;
-  }
-  __device__ __forceinline__ int nx() const { return n_x; }
-  __device__ __forceinline__ double wx() const { return w_x; }
-  // after a backup: x visited once more with value share dv, p once more
-  __device__ __forceinline__ void update(double dv) {
-    const int lane = lane_id_local();
-    n_x += 1;
-    w_x = w_x + dv;
-    if (lane == (x & 63)) {
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j)
-        if (j == (x >> 6)) m.n[j][lane] = n_x;
-    }
-    N += 1;
-    renorm(false);
-  }
-};
 
 // ---------------------------------------------------------------------------
 // select_leaf (self_play.py:239-335).  Wave 0.  Returns the action to expand
