@@ -63,7 +63,7 @@ struct ExpandLds {
     double db[64 * G::AP];
   };
   Wave wv[BATCH ? G::WAVES : 1];          // (after the batch: verify_batch's arrays)
-  double bv[BATCH ? G::A : 1];            // backup value of each batched child
+  double bv[BATCH ? G::A + 16 : 1];       // backup value of each batched child (+ tail read by prefix_sums)
   int acts[BATCH ? G::A : 1];             // action of each batched child
 };
 

@@ -454,23 +454,58 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
 // and first-maximum rule; the batch is accepted up to the first failing i,
 // and the tree takes the accepted simulations' sums.  Returns the number of
 // accepted simulations m >= 1 (all threads; synchronised).
+// dst[0] = w0, dst[k + 1] = dst[k] + (neg ? -v[k] : v[k]) for k < B: the
+// sequential f64 sums (lane 0), 8 at a time without branches, the next 8
+// loads in flight: v is read up to 15 and dst written up to 7 entries past B
+// (those sums are never read).  Wave-level.
+template <class G>
+__device__ __forceinline__ void prefix_sums(double w0, const double* __restrict__ v, int B, bool neg,
+                                            double* __restrict__ dst) {
+  if (lane_id_local() == 0) {
+    double w = w0;
+    dst[0] = w;
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = v[u];
+    for (int k0 = 0; k0 < B; k0 += 8) {
+      double y[8];                                 // the next chunk's loads, in flight during the chain
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[u] = v[k0 + 8 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        w = w + (neg ? -x[u] : x[u]);
+        dst[k0 + u + 1] = w;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = y[u];
+    }
+  }
+}
+
 template <class G, int DMAX>
 struct VerifyLds {
   double cP[DMAX][64 * G::AP];      // c_puct * P as puct_pick forms it
   double q[DMAX][64 * G::AP];       // W / N of every child, now
+  double inv1n[DMAX][64 * G::AP];   // 1 / (1 + N) of every child, now (the screening pass)
   int n[DMAX][64 * G::AP];
+  // per (level, i): x's q after i accepted simulations, 1 / (hi - lo) of the
+  // level's q range then (0: no spread), the sqrt term, and x's exact score
+  double qx[DMAX][G::A + 1], invr[DMAX][G::A + 1], sq[DMAX][G::A + 1], sx[DMAX][G::A + 1];
   uint64_t elig[DMAX][G::AP];
   double lo_o[DMAX], hi_o[DMAX];    // min / max of q over eligible children other than x
   int x[DMAX], n0[DMAX], N0[DMAX];
-  double wpre[DMAX][G::A + 1];      // x_l's value sum after i accepted simulations
-  double wroot[G::A + 1];           // the root's value sum after i
+  double wpre[DMAX][G::A + 9];      // x_l's value sum after i accepted simulations (+ prefix_sums' tail)
+  double wroot[G::A + 9];           // the root's value sum after i
+  uint64_t badm[DMAX][G::AP];       // simulations i whose x score is not finite at level l
+  uint64_t failm[G::AP];            // simulations i whose walk leaves the batch (bit i)
+  uint64_t exactm[DMAX][G::AP];     // (level, i) checks the screening left open
   int fail;
 };
-constexpr int kVerifyDepth = 12;
+constexpr int kVerifyDepth = 8;     // deeper paths replay one select at a time
 
 template <class G, class Acc>
 __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, Acc& T,
-                                            int* nact, int leaf, int D, int B, int nid) {
+                                            int* nact, int leaf, int D, int B, int nid, Stamp* st = nullptr) {
   if constexpr (!decltype(sm.u.f)::BATCH) {
     return 0;                                       // (no speculative batches without the batch LDS)
   } else {
@@ -481,23 +516,18 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   const int lane = lane_id_local();
   const bool alt = sp.variant == 0;
   const double* bv = sm.u.f.bv;
-  // share of the node at depth d in a batch child's backup: v (-1)^(D + 1 - d)
-  auto share = [&](int d, double v) { return alt && ((D + 1 - d) & 1) ? -v : v; };
-  if (threadIdx.x == 0) vl.fail = B;
+  // the node at depth d takes the share v (-1)^(D + 1 - d) of a batch child's backup
+  if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
+  if (threadIdx.x < kVerifyDepth * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
   // ---- 1. the levels (one wave each) and the root's own sums ----
   for (int l = wave; l <= D; l += G::WAVES) {
     if (l == D) {                                   // the root's value sum after i simulations
-      if (lane == 0) {
-        double w = T.ws(0);
-        vl.wroot[0] = w;
-        for (int k = 0; k < B - 1; ++k) { w = w + share(0, bv[k]); vl.wroot[k + 1] = w; }
-        vl.wroot[B] = w + share(0, bv[B - 1]);
-      }
+      prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
       continue;
     }
     const int p = T.path(l);
     const int xa = l == 0 ? sm.t.ract : nact[T.path(l + 1)];
-    double lo = INFINITY, hi = -INFINITY, wx = 0.0;
+    double lo = INFINITY, hi = -INFINITY, wx = 0.0, cpx = 0.0;
     int nx = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
@@ -516,61 +546,171 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
       const bool e = P > 0.0;
       const uint64_t el = __ballot(e);
       const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
-      vl.cP[l][a] = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
+      const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
+      vl.cP[l][a] = cp;
       vl.q[l][a] = q;
+      vl.inv1n[l][a] = 1.0 / (double)(1 + n);
       vl.n[l][a] = n;
       if (lane == 0) vl.elig[l][j] = el;
       if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
-      if (j == (xa >> 6)) { wx = dpp::lane(w, xa & 63); nx = __builtin_amdgcn_readlane(n, xa & 63); }
+      if (j == (xa >> 6)) {
+        wx = dpp::lane(w, xa & 63);
+        nx = __builtin_amdgcn_readlane(n, xa & 63);
+        cpx = dpp::lane(cp, xa & 63);
+      }
     }
     wave_minmax(lo, hi);
+    if (st) st->lap(75);
+    const int N0 = T.vis(p);
     if (lane == 0) {
       vl.lo_o[l] = lo;
       vl.hi_o[l] = hi;
       vl.x[l] = xa;
       vl.n0[l] = nx;
-      vl.N0[l] = T.vis(p);
-      double w = wx;                                // x_l = p_(l+1): depth l + 1
-      vl.wpre[l][0] = w;
-      for (int k = 0; k < B; ++k) { w = w + share(l + 1, bv[k]); vl.wpre[l][k + 1] = w; }
+      vl.N0[l] = N0;
     }
+    prefix_sums<G>(wx, bv, B, alt && ((D - l) & 1), vl.wpre[l]);   // x_l = p_(l+1): depth l + 1
+    wave_lds_sync();
+    if (st) st->lap(76);
+    // per simulation i (lane i = lane + 64 j): the level as simulation i's
+    // select finds it, and x's score exactly as puct_pick forms it
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int i = lane + 64 * j;
+      bool bad = false;
+      if (i <= B) {
+        const int n1 = nx + i, Ni = N0 + i;
+        const double qxi = n1 > 0 ? vl.wpre[l][i] / (double)n1 : 0.0;
+        const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
+        const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
+        const double sxi = (hii > loi ? (qxi - loi) / (hii - loi) : qxi) + (cpx * sqi) / (double)(1 + n1);
+        vl.qx[l][i] = qxi;
+        vl.invr[l][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;
+        vl.sq[l][i] = sqi;
+        vl.sx[l][i] = sxi;
+        bad = i >= 1 && i < B && !(sxi > -INFINITY);
+      }
+      const uint64_t bb = __ballot(bad);
+      if (lane == 0) vl.badm[l][j] = bb;
+    }
+    if (st) st->lap(77);
   }
   __syncthreads();
-  // ---- 2. every (i, l) check at once ----
-  const int items = (B - 1) * D;
-  for (int it = wave; it < items; it += G::WAVES) {
-    const int i = 1 + it / D, l = it - (i - 1) * D;
-    if (__hip_atomic_load(&vl.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= i) continue;
+  if (st) st->lap(72);
+  // ---- 2. every (i, l) check at once, transposed: lanes are simulations
+  // i = lane + 64 j, each wave takes every WAVES-th child a of each level.
+  // Screening: the two divisions of a's score as products with reciprocals
+  // (a few ulp off); a decides (l, i) only if its score is clear of x's by
+  // far more than that, else (l, i) is redone below with puct_pick's exact
+  // operations.  i fails if any eligible a != x beats x (puct_pick's first
+  // maximum: a higher score, or an equal one at a lower action). ----
+  const unsigned long long ts0 = st ? st->now() : 0;
+  for (int l = 0; l < D; ++l) {
     const int xa = vl.x[l];
-    const int nx = vl.n0[l] + i, N = vl.N0[l] + i;
-    const double qx = nx > 0 ? vl.wpre[l][i] / (double)nx : 0.0;
-    const double lo = fmin(vl.lo_o[l], qx), hi = fmax(vl.hi_o[l], qx);
-    const double sq = sp.variant == 1 ? sqrt((double)(N + 1)) : sqrt((double)(N > 1 ? N : 1));
-    double sc[G::AP];
-    bool el[G::AP];
+    const double lo_o = vl.lo_o[l], hi_o = vl.hi_o[l];
+    double loi[G::AP], invr[G::AP], sqi[G::AP], sxi[G::AP], tol[G::AP];
+    bool spread[G::AP];
+    uint64_t beaten[G::AP], close[G::AP];
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      el[j] = (vl.elig[l][j] >> lane) & 1ull;
-      const bool isx = a == xa;
-      const double q = isx ? qx : vl.q[l][a];
-      const int n = isx ? nx : vl.n[l][a];
-      const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
-      sc[j] = qn + (vl.cP[l][a] * sq) / (double)(1 + n);
+      const int i = lane + 64 * j;
+      const int ii = i <= B ? i : B;
+      const double qxi = vl.qx[l][ii];
+      loi[j] = fmin(lo_o, qxi);
+      spread[j] = fmax(hi_o, qxi) > loi[j];
+      invr[j] = vl.invr[l][ii];
+      sqi[j] = vl.sq[l][ii];
+      sxi[j] = vl.sx[l][ii];
+      tol[j] = 1e-12 * (1.0 + fabs(sxi[j]));
+      beaten[j] = 0;
+      close[j] = 0;
     }
-    double sx = 0.0;
+    // the wave's children a = wave + WAVES k, one per lane k, loaded in one
+    // round trip; the loop broadcasts them with readlane
+    constexpr int KW = (G::A + G::WAVES - 1) / G::WAVES;
+    static_assert(KW <= 64, "one lane per child of the wave");
+    const int amine = wave + G::WAVES * lane;
+    const bool mine = lane < KW && amine < G::A && amine != xa &&
+                      ((vl.elig[l][(amine < G::A ? amine : 0) >> 6] >> (amine & 63)) & 1ull);
+    const int ac = mine ? amine : 0;
+    const double qa_l = vl.q[l][ac], cpa_l = vl.cP[l][ac], ia_l = vl.inv1n[l][ac];
+    const uint64_t todo = __ballot(mine);
+    for (uint64_t mm = todo; mm; mm &= mm - 1) {
+      const int k = __builtin_ctzll(mm);
+      const double qa = dpp::lane(qa_l, k), cpa = dpp::lane(cpa_l, k), ia = dpp::lane(ia_l, k);
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (j == (xa >> 6)) sx = dpp::lane(sc[j], xa & 63);
-    uint64_t beat = 0;
+      for (int j = 0; j < G::AP; ++j) {
+        if (64 * j >= B) break;                     // (uniform) no simulation i in this register
+        const double sc = (spread[j] ? (qa - loi[j]) * invr[j] : qa) + (cpa * sqi[j]) * ia;
+        beaten[j] |= __ballot(sc > sxi[j] + tol[j]);
+        close[j] |= __ballot(!(fabs(sc - sxi[j]) > tol[j]));
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        if (beaten[j]) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)beaten[j]);
+        if (close[j] & ~beaten[j])
+          atomicOr(reinterpret_cast<unsigned long long*>(&vl.exactm[l][j]), (unsigned long long)(close[j] & ~beaten[j]));
+      }
+    }
+  }
+  if (st) st->wave_add(80, st->now() - ts0);
+  __syncthreads();
+  if (st) st->lap(78);
+  // the open (l, i) checks with puct_pick's exact operations (rare)
+  for (int l = 0; l < D; ++l) {
+    uint64_t open[G::AP];
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      beat |= __ballot(el[j] && a != xa && (sc[j] > sx || (sc[j] == sx && a < xa)));
+      const uint64_t o = vl.exactm[l][j] & ~vl.failm[j];
+      open[j] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t)o);
     }
-    if ((beat != 0 || !(sx > -INFINITY)) && lane == 0) atomicMin(&vl.fail, i);
+    int k = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      for (uint64_t mm = open[j]; mm; mm &= mm - 1, ++k) {
+        if (k % G::WAVES != wave) continue;
+        const int i = 64 * j + __builtin_ctzll(mm);
+        if (i < 1 || i >= B) continue;
+        const int xa = vl.x[l];
+        const int nx = vl.n0[l] + i;
+        const double qx = vl.qx[l][i];
+        const double lo = fmin(vl.lo_o[l], qx), hi = fmax(vl.hi_o[l], qx);
+        const double sq = vl.sq[l][i], sx = vl.sx[l][i];
+        uint64_t beat = 0;
+#pragma unroll
+        for (int jj = 0; jj < G::AP; ++jj) {
+          const int a = lane + 64 * jj;
+          const bool el = (vl.elig[l][jj] >> lane) & 1ull;
+          const bool isx = a == xa;
+          const double q = isx ? qx : vl.q[l][a];
+          const int n = isx ? nx : vl.n[l][a];
+          const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
+          const double sc = qn + (vl.cP[l][a] * sq) / (double)(1 + n);
+          beat |= __ballot(el && !isx && (sc > sx || (sc == sx && a < xa)));
+        }
+        if (beat && lane == 0)
+          atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[i >> 6]), 1ull << (i & 63));
+      }
+    }
   }
   __syncthreads();
+  if (st) st->lap(79);
+  if (threadIdx.x == 0) {
+    int f = B;
+#pragma unroll
+    for (int j = G::AP - 1; j >= 0; --j) {
+      uint64_t mm = vl.failm[j];
+      for (int l = 0; l < D; ++l) mm |= vl.badm[l][j];
+      if (j == 0) mm &= ~1ull;                         // (simulation i = 0 reached the leaf already)
+      if (mm) f = 64 * j + __builtin_ctzll(mm);
+    }
+    vl.fail = f < B ? f : B;
+  }
+  __syncthreads();
+  if (st) st->lap(73);
   const int m = vl.fail;
   // ---- 3. the tree takes the m accepted simulations ----
   if (wave_id() == 0) {
@@ -595,6 +735,7 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
     if (lane == 0) { sm.t.newest = -1; sm.t.ycache = leaf; }
   }
   __syncthreads();
+  if (st) st->lap(74);
   return m;
   }
 }
@@ -709,7 +850,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         __syncthreads();
         st.lap(5);
         if (Acc::LDS && depth <= kVerifyDepth) {
-          const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid);
+          const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
           nodes += m;
           sim += m;
           st.lap(63);

@@ -73,7 +73,7 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 72), np.uint64)
+    buf = np.zeros((G, 88), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
@@ -100,6 +100,10 @@ def stamps_report():
                       "expand_per_child_copyE_heads_logits_priors": [round(float(allp[i] / max(allp[68], 1e-9)))
                                                                      for i in (64, 65, 66, 67)],
                       "expanded_children_per_search": float(allp[68] * S),
+                      "verify_steps_total": [round(float(allp[i]) * S) for i in (72, 73, 74)],
+                      "verify_step2_main_exact": [round(float(allp[i]) * S) for i in (78, 79)],
+                      "verify_step2_loop_all_waves": round(float(allp[80]) * S),
+                      "verify_step1_w0_pre_minmax_prefix_reciprocals": [round(float(allp[i]) * S) for i in (75, 76, 77)],
                       "batch_end_barrier_total": round(float(allp[63]) * 2 * S / 2),
                       "batches_per_search": float(buf[:, 31].astype(np.float64).mean() / 2),
                       "batched_sims_per_search": float(buf[:, 28].astype(np.float64).mean() / 2),
