@@ -14,11 +14,12 @@
 #include "mzgo_dispatch.hpp"
 
 namespace mzgo {
-extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96, kernels_n6_c128;
+extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96, kernels_n6_c128,
+    kernels_n6_c64;
 
 const KernelSet* find_kernels(int N, int C) {
   static const KernelSet* all[] = {&kernels_n5_c96, &kernels_n6_c96, &kernels_n9_c96, &kernels_n19_c96,
-                                   &kernels_n6_c128};
+                                   &kernels_n6_c128, &kernels_n6_c64};
   for (const KernelSet* k : all)
     if (k->N == N && k->C == C) return k;
   return nullptr;
@@ -312,7 +313,7 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   *out = nullptr;
   const int N = cfg->board_size, C = cfg->latent_dim;
   const KernelSet* ks = find_kernels(N, C == 0 ? 96 : C);
-  if (!ks) return fail(MZGO_EINVAL, "unsupported board_size %d / latent_dim %d (built: N in {5,6,9,19} with C=96; N=6 with C=128)", N, C);
+  if (!ks) return fail(MZGO_EINVAL, "unsupported board_size %d / latent_dim %d (built: N in {5,6,9,19} with C=96; N=6 with C=128 or 64)", N, C);
   if (cfg->num_games < 1) return fail(MZGO_EINVAL, "num_games must be >= 1");
   if (C != 0 && cfg->num_simulations < 1) return fail(MZGO_EINVAL, "num_simulations must be >= 1");
   if (cfg->compat != 0 && cfg->compat != 1) return fail(MZGO_EINVAL, "compat must be 0 or 1");

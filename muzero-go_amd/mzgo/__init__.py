@@ -10,6 +10,7 @@ self_play.py), all executed by libmzgo.so's HIP kernels:
 * ``SelfPlay``    -- G concurrent games per GPU, one fused kernel step per move
 * ``SelfPlayEvaluator`` -- main.py's arena (two networks, all games at once)
 * ``GameHistory``, ``save_batches`` -- the reference's record / pickle format
+* ``mzgo.play`` -- play.py's interactive human-vs-agent loop (``python -m mzgo.play weights.pth``)
 """
 from .arena import SelfPlayEvaluator
 from .engine import Engine, EngineConfig

@@ -101,6 +101,8 @@ class Engine:
         """Load reference state_dict tensors (any device/dtype -> host f32)."""
         for key, t in state_dict.items():
             a = np.ascontiguousarray(torch.as_tensor(t).detach().to("cpu", torch.float32).numpy())
+            if key == "dynamics.action_embedding.weight" and a.ndim == 2 and a.shape[0] > self.A:
+                a = np.ascontiguousarray(a[:self.A])      # rows past the board's actions (play.py:193)
             shape = (ctypes.c_int64 * a.ndim)(*a.shape)
             check(lib.mzgo_set_weights(self._h, key.encode(), ptr(a), shape, a.ndim))
         if not lib.mzgo_weights_ready(self._h):

@@ -51,11 +51,21 @@ def board_size_of(action_size):
 
 
 class MuZeroNet(nn.Module):
-    def __init__(self, latent_dim, max_action_size):
+    """``board_size``: for networks whose embedding table is larger than the
+    board's N*N+1 actions (play.py:193 sizes it int(1.5 N^2)); the extra rows
+    are kept in the state_dict and never reach the engine (actions >= N*N+1
+    do not exist on the board)."""
+
+    def __init__(self, latent_dim, max_action_size, board_size=None):
         super().__init__()
         self.latent_dim = latent_dim
         self.max_action_size = max_action_size
-        self.board_size = board_size_of(max_action_size)
+        if board_size is None:
+            self.board_size = board_size_of(max_action_size)
+        else:
+            if max_action_size < board_size * board_size + 1:
+                raise ValueError(f"max_action_size {max_action_size} < {board_size}*{board_size}+1 actions")
+            self.board_size = board_size
         self.representation = _Representation(latent_dim)
         self.dynamics = _Dynamics(latent_dim, max_action_size)
         self.prediction = _Prediction(latent_dim)

@@ -66,8 +66,8 @@ class MCTS:
         if not isinstance(muzero_net, MuZeroNet):
             raise TypeError("mzgo.MCTS searches with an mzgo.MuZeroNet (HIP engine); got "
                             f"{type(muzero_net).__name__}")
-        if action_size != muzero_net.max_action_size:
-            raise ValueError("action_size must equal the net's max_action_size")
+        if action_size != muzero_net.board_size ** 2 + 1:
+            raise ValueError("action_size must be the board's N*N+1 actions")
         self.net = muzero_net
         self.action_size = action_size
         self.num_simulations = num_simulations

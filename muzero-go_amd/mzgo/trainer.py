@@ -246,7 +246,7 @@ class MuZeroTrainer:
         self.net = net
         self.config = config or TrainConfig()
         self.mode = mode
-        self.action_size = net.max_action_size
+        self.action_size = net.board_size ** 2 + 1
         self.optimizer = torch.optim.Adam(net.parameters(), lr=self.config.learning_rate)
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=self.config.lr_step_size,
                                                          gamma=self.config.lr_gamma)
