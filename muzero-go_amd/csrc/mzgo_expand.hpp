@@ -270,7 +270,8 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
 // -> dst [C][CS] (channel-major, pad cells 0), the layout the 3x3 conv reads.
 // Y is cell-major, so 32-channel slabs are transposed through LDS (lds: at
 // least 32 * (CS + 1) floats, free until the conv): coalesced reads and
-// writes.  All threads; returns synchronised.
+// writes.  (One round over all channels at once measured slower.)  All
+// threads; returns synchronised.
 template <class G>
 __device__ __forceinline__ void materialize(float* __restrict__ dst, const float* __restrict__ Ypar,
                                             const float* __restrict__ ea, float* lds) {

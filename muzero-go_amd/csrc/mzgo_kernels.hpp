@@ -811,9 +811,11 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           materialize<G>(scratch, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
                          sm.ulds());
         }
+        st.lap(81);
         latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS, G::CS,
                                             nullptr, &st);
         __syncthreads();                                 // Y stores before the expansion reads them
+        st.lap(82);
         yc = -1;                                         // the conv overwrote the LDS copy
         if (threadIdx.x == 0) { st.wave_add(59, 1); ++convs; }   // convs run
       }

@@ -103,6 +103,7 @@ def stamps_report():
                       "verify_steps_total": [round(float(allp[i]) * S) for i in (72, 73, 74)],
                       "verify_step2_main_exact": [round(float(allp[i]) * S) for i in (78, 79)],
                       "verify_step2_loop_all_waves": round(float(allp[80]) * S),
+                      "parent_materialize_and_conv_tail": [round(float(allp[i]) * S) for i in (81, 82)],
                       "verify_step1_w0_pre_minmax_prefix_reciprocals": [round(float(allp[i]) * S) for i in (75, 76, 77)],
                       "batch_end_barrier_total": round(float(allp[63]) * 2 * S / 2),
                       "batches_per_search": float(buf[:, 31].astype(np.float64).mean() / 2),
