@@ -45,22 +45,33 @@ struct ExpandShape {
 // and, if they fit, a copy of one node's Y and of the 1x1 head weights (so
 // that consecutive expansions of the same leaf read them from LDS instead of
 // L2; a conv overwrites the union and the next expansion refills it), and
-// the per-wave buffers of the batched root phase (root_batch).
+// the per-wave buffers of the batches (batch_expand).  Boards whose Y does
+// not fit (19x19) still batch, each wave streaming Y from L2 (GLOBAL_Y) with
+// smaller per-wave buffers: the policy row only, E[a], and E's space reused
+// as the ordered-sum scratch of child_priors.
 template <class G, int UF>
 struct ExpandLds {
   static constexpr int YC = G::CELLS * G::C;
   static constexpr int BASE = YC + 3 * G::CS + 3 * G::C;
   static constexpr bool CACHE = BASE <= UF;
   static constexpr int PERW = 3 * G::CS + 9 * G::C + 3 * 64 * G::AP;   // one wave's batch buffers
-  static constexpr bool BATCH = CACHE && BASE + G::WAVES * PERW + 3 * G::A + 64 <= UF;
+  static constexpr int PERW_G = G::CS + 9 * G::C;                      // ... with Y streamed from L2
+  static_assert(CACHE || 9 * G::C >= 2 * 64 * G::AP, "E's space holds child_priors' scratch (f32 then f64, in turn)");
+  static constexpr bool BATCH = CACHE ? BASE + G::WAVES * PERW + 3 * G::A + 64 <= UF
+                                      : 3 * G::CS + 3 * G::C + G::WAVES * PERW_G + 3 * G::A + 64 <= UF;
+  static constexpr bool GLOBAL_Y = BATCH && !CACHE;
+  static constexpr int XW = CACHE ? 3 * G::CS : G::CS;   // a wave's head rows; the policy row at PROW
+  static constexpr int PROW = CACHE ? 2 * G::CS : 0;
   alignas(16) float yc[CACHE ? YC : 4];
-  alignas(16) float hw[CACHE ? 3 * G::C : 4];
+  alignas(16) float hw[CACHE || BATCH ? 3 * G::C : 4];
   float xh[3 * G::CS];
   struct Wave {
-    alignas(16) float xw[3 * G::CS];      // the child's head sums
+    alignas(16) float xw[XW];             // the child's policy sums per cell (at PROW)
     alignas(16) float ew[9 * G::C];       // E[a] of the child
-    float fb[64 * G::AP];                 // ordered-sum scratch (child_priors)
-    double db[64 * G::AP];
+    float fb[CACHE ? 64 * G::AP : 1];     // ordered-sum scratch (child_priors)
+    double db[CACHE ? 64 * G::AP : 1];
+    __device__ float* fscratch() { if constexpr (CACHE) return fb; else return ew; }
+    __device__ double* dscratch() { if constexpr (CACHE) return db; else return reinterpret_cast<double*>(ew); }
   };
   Wave wv[BATCH ? G::WAVES : 1];          // (after the batch: verify_batch's arrays)
   double bv[BATCH ? G::A + 16 : 1];       // backup value of each batched child (+ tail read by prefix_sums)
@@ -176,26 +187,37 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
 template <class G>
 struct ExpandPlan {
   static constexpr int PASSES = (G::CELLS + 7) / 8;
-  uint32_t off[(PASSES + 1) / 2];
+  static constexpr bool TABLE = PASSES <= 16;         // else (19x19) each pass works its region out
+  uint32_t off[TABLE ? (PASSES + 1) / 2 : 1];
   static_assert(8 * PASSES <= G::CS, "the last pass's cells stay inside the head rows");
   static_assert(8 * 4 * G::C < 65536, "16-bit region offsets");
   __device__ __forceinline__ void init() {
-    const int cg = lane_id_local() >> 3;
+    if constexpr (TABLE) {
+      const int cg = lane_id_local() >> 3;
 #pragma unroll
-    for (int i = 0; i < (PASSES + 1) / 2; ++i) off[i] = 0;
+      for (int i = 0; i < (PASSES + 1) / 2; ++i) off[i] = 0;
 #pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int cell = cg + 8 * p;
-      const uint32_t reg = cell < G::CELLS ? (uint32_t)region_of<G>(cell) : 0u;
-      off[p >> 1] |= (reg * (uint32_t)G::C * 4u) << (16 * (p & 1));
+      for (int p = 0; p < PASSES; ++p) {
+        const int cell = cg + 8 * p;
+        const uint32_t reg = cell < G::CELLS ? (uint32_t)region_of<G>(cell) : 0u;
+        off[p >> 1] |= (reg * (uint32_t)G::C * 4u) << (16 * (p & 1));
+      }
     }
   }
-  __device__ __forceinline__ uint32_t at(int p) const { return (off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu; }
+  __device__ __forceinline__ uint32_t at(int p) const {
+    if constexpr (TABLE) {
+      return (off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu;
+    } else {
+      const int cell = (lane_id_local() >> 3) + 8 * p;
+      return cell < G::CELLS ? (uint32_t)region_of<G>(cell) * (uint32_t)G::C * 4u : 0u;
+    }
+  }
 };
 
-// One child's heads by ONE wave (batch_expand), Y [CELLS][C], E[a] [9][C]
-// and the head weights hw [3][C] (reward, value, policy) all in LDS:
-//   * the policy 1x1-conv sum of relu(Y + E[a]) per cell -> xw[2][cell];
+// One child's heads by ONE wave (batch_expand), Y [CELLS][C] (LDS, or L2 for
+// GLOBAL_Y boards), E[a] [9][C] and the head weights hw [3][C] (reward,
+// value, policy) in LDS:
+//   * the policy 1x1-conv sum of relu(Y + E[a]) per cell -> xw[PROW + cell];
 //   * the reward and value heads only enter the network through their means
 //     over the cells (self_play.py:91-94, :105-110), and a 1x1 conv is
 //     linear, so their totals are taken channel-first:
@@ -208,7 +230,7 @@ struct ExpandPlan {
 // same address), so no lane is masked off; the last pass's cells past the
 // board land in the row padding and stay out of S.  Wave-level; the caller
 // orders xw for the wave's readers (wave_lds_sync).
-template <class G>
+template <class G, int PROW>
 __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw,
                                             const ExpandPlan<G>& plan, float& rsum, float& vsum) {
   typedef ExpandShape<G> X;
@@ -226,8 +248,9 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   }
   const f32x4* Y4 = reinterpret_cast<const f32x4*>(yc) + cg * X::C4 + j;   // + pass * 8 * C4 + 8 k
   const char* Eb = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew) + j);
-  float* xr = xw + 2 * G::CS + cg;
-#pragma unroll
+  float* xr = xw + PROW + cg;
+  // every pass unrolled on small boards; two at a time on 19x19 (46 passes)
+#pragma unroll (P <= 16 ? P : 2)
   for (int p = 0; p < P; ++p) {
     const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + plan.at(p));
     f32x4 y[X::PERL], e[X::PERL];

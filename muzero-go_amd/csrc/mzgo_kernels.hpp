@@ -267,9 +267,11 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
 // joins).  All threads; the caller synchronises.
 template <class G, bool LAZY>
 __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
-                                             const TreeView& TV, int B, int nid0, Stamp* st = nullptr) {
+                                             const TreeView& TV, int B, int nid0, const float* yg,
+                                             Stamp* st = nullptr) {
   auto& L = sm.u.f;
-  if constexpr (decltype(sm.u.f)::BATCH) {
+  typedef decltype(sm.u.f) XL;
+  if constexpr (XL::BATCH) {
     const int wave = __builtin_amdgcn_readfirstlane(wave_id());
     const int lane = lane_id_local();
     auto& W = L.wv[wave];
@@ -304,7 +306,8 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
       wave_lds_sync();
       if (st) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
       float rsum, vsum;
-      expand_wave<G>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
+      if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+      else expand_wave<G, XL::PROW>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
       wave_lds_sync();
       epre_a = -1;
       kn = grab();
@@ -319,7 +322,7 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
       if (st) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
       float r, v, x[G::AP];
       heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
-      logits_regs<G, 1>(W.xw, true, sm.t.hsc, x);
+      policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
       int* crow = TV.child + (size_t)nid * G::A;
       for (int i = lane; i < G::A; i += 64) crow[i] = -1;
       if (st) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
@@ -332,7 +335,7 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
           if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
         if (lane == 0) atomicOr(&sm.t.rawp[nid >> 5], 1u << (nid & 31));
       } else {
-        child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fb, W.db);
+        child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
       }
       if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
       wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
@@ -341,17 +344,20 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
   }
 }
 
-// Node n's Y (global, [CELLS][C]) and the head weights into the LDS copies.
-// All threads; the caller synchronises.
+// Node n's Y (global, [CELLS][C]) and the head weights into the LDS copies
+// (GLOBAL_Y boards: the head weights only).  All threads; the caller
+// synchronises.
 template <class G>
 __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float* head_w) {
   auto& L = sm.u.f;
-  if constexpr (decltype(sm.u.f)::CACHE) {
+  typedef decltype(sm.u.f) XL;
+  if constexpr (XL::CACHE) {
     const f32x4* src = reinterpret_cast<const f32x4*>(y);
     f32x4* dst = reinterpret_cast<f32x4*>(L.yc);
     for (int i = threadIdx.x; i < G::CELLS * G::C / 4; i += G::THREADS) dst[i] = src[i];
-    for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
   }
+  if constexpr (XL::CACHE || XL::BATCH)
+    for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
 }
 
 // Batched root phase.  While the root has unexpanded eligible children,
@@ -409,7 +415,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       }
       pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
     }
-    batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, st);
+    batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, pool, st);
     __syncthreads();
     if (st) st->lap(62);
     if (wave_id() == 0) {
@@ -848,16 +854,18 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1);
           st.lap(71);
         }
-        batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, &st);
+        batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
         __syncthreads();
         st.lap(5);
-        if (Acc::LDS && depth <= kVerifyDepth) {
-          const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
-          nodes += m;
-          sim += m;
-          st.lap(63);
-          if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
-          continue;
+        if constexpr (Acc::LDS) {
+          if (depth <= kVerifyDepth) {
+            const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
+            nodes += m;
+            sim += m;
+            st.lap(63);
+            if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
+            continue;
+          }
         }
         if (wave_id() == 0) {
           const int lane = lane_id_local();

@@ -309,6 +309,20 @@ __device__ __forceinline__ void logits_regs(const float* hp, bool has_reward, co
   }
 }
 
+// policy logits from one row of policy 1x1-conv sums (no bias) per cell: a
+// lane's actions a = lane + 64 j (cells, then the learned pass logit).  One
+// wave.
+template <class G>
+__device__ __forceinline__ void policy_logits(const float* row, const float* hsc, float (&x)[G::AP]) {
+  const int lane = lane_id_local();
+  const float pb = hsc[HS_PB];
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    x[j] = a < G::CELLS ? row[a] + pb : hsc[HS_PASS];
+  }
+}
+
 // policy logits -> logits[A] (LDS).  One wave.
 template <class G, int NPART>
 __device__ __forceinline__ void heads_logits(const float* hp, bool has_reward, const float* hsc, float* logits) {
