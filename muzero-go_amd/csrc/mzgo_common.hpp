@@ -77,8 +77,9 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // 0-7 phases (thread 0), 8-19 per-wave conv loops, 20-31 sub-phases,
 // 32-43 per-wave conv-input work, 44-55 per-wave conv-input barrier wait,
 // 56-63 factored simulation detail (see sim_loop), 64-71 batch_expand detail,
-// 72-87 verify_batch steps
-constexpr int kStampPhases = 88;
+// 72-82 verify_batch / parent conv detail, 83-87 self-play move phases,
+// 88-90 representation convs
+constexpr int kStampPhases = 91;
 #ifdef MZGO_STAMPS
 // Phase sums accumulate in LDS (a global read-modify-write per lap would put
 // an HBM round trip on the measured wave's critical path); flush() adds them

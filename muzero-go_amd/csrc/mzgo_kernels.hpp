@@ -174,7 +174,7 @@ constexpr bool rep_needs_scratch() {
 
 template <class G, class PlaneFn>
 __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
-                                      int lat_stride, float* scr) {
+                                      int lat_stride, float* scr, unsigned long long* ts = nullptr) {
   float* mid = rep_needs_scratch<G>() ? scr : lat;
   for (int i = threadIdx.x; i < 6 * G::CELLS; i += G::THREADS) {
     const int c = i / G::CELLS, j = i - c * G::CELLS;
@@ -187,8 +187,14 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
   const int oc = lat_stride == G::CS ? G::CS : G::CELLS;   // pooled latents also write their 0 pads
   conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
   __syncthreads();
+#ifdef MZGO_STAMPS
+  if (ts) ts[0] = __builtin_amdgcn_s_memtime();
+#endif
   latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, mid, lat_stride, oc, nullptr);
   __syncthreads();                                         // conv2's stores before conv3 reads them
+#ifdef MZGO_STAMPS
+  if (ts) ts[1] = __builtin_amdgcn_s_memtime();
+#endif
   latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, mid, lat_stride, nullptr, lat, lat_stride, oc,
                               np.head_w + G::C);
   if (wave_id() == 0)
@@ -507,7 +513,10 @@ struct VerifyLds {
   uint64_t exactm[DMAX][G::AP];     // (level, i) checks the screening left open
   int fail;
 };
-constexpr int kVerifyDepth = 8;     // deeper paths replay one select at a time
+// leaf depths verify_batch handles (its arrays are per level; deeper paths
+// replay one select at a time): 8 at 9x9 and below, 2 at 19x19 (A = 362)
+template <class G>
+constexpr int verify_depth() { return G::AP > 2 ? 2 : 8; }
 
 template <class G, class Acc>
 __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, Acc& T,
@@ -515,7 +524,8 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   if constexpr (!decltype(sm.u.f)::BATCH) {
     return 0;                                       // (no speculative batches without the batch LDS)
   } else {
-  typedef VerifyLds<G, kVerifyDepth> V;
+  constexpr int DV = verify_depth<G>();
+  typedef VerifyLds<G, DV> V;
   static_assert(sizeof(V) <= sizeof(sm.u.f.wv), "verification arrays overlay the batch buffers");
   V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
@@ -524,7 +534,7 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   const double* bv = sm.u.f.bv;
   // the node at depth d takes the share v (-1)^(D + 1 - d) of a batch child's backup
   if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
-  if (threadIdx.x < kVerifyDepth * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
+  if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
   // ---- 1. the levels (one wave each) and the root's own sums ----
   for (int l = wave; l <= D; l += G::WAVES) {
     if (l == D) {                                   // the root's value sum after i simulations
@@ -543,7 +553,12 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
       int n = 0;
       if (l == 0) {
         P = in ? T.root_prior(a) : 0.0;
-        if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }
+        if constexpr (Acc::LDS) {
+          if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
+        } else {
+          const int c = in ? T.child(0, a) : -1;
+          if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+        }
       } else {
         P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
         const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
@@ -726,7 +741,8 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
       } else {
         const int l = lane - 1;                     // p_lane = x_l
         T.set(T.path(lane), vl.n0[l] + m, vl.wpre[l][m]);
-        if (lane == 1) { sm.t.rvis[sm.t.ract] = vl.n0[0] + m; sm.t.rws[sm.t.ract] = vl.wpre[0][m]; }
+        if constexpr (Acc::LDS)
+          if (lane == 1) { sm.t.rvis[sm.t.ract] = vl.n0[0] + m; sm.t.rws[sm.t.ract] = vl.wpre[0][m]; }
       }
     }
     wave_lds_sync();
@@ -857,15 +873,13 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
         __syncthreads();
         st.lap(5);
-        if constexpr (Acc::LDS) {
-          if (depth <= kVerifyDepth) {
-            const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
-            nodes += m;
-            sim += m;
-            st.lap(63);
-            if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
-            continue;
-          }
+        if (depth <= verify_depth<G>()) {
+          const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
+          nodes += m;
+          sim += m;
+          st.lap(63);
+          if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
+          continue;
         }
         if (wave_id() == 0) {
           const int lane = lane_id_local();
@@ -962,7 +976,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
 template <class G, class PlaneFn>
 __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                   const EngineArrays& E, int g, PlaneFn planes, const double* noise,
-                                  uint64_t key) {
+                                  uint64_t key, unsigned long long* ts = nullptr) {
   const TreeView TV = TreeViewOf<G>::make(E, g);
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
   float* pool = pool_of<G>(E, g);
@@ -970,11 +984,17 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
   // root latent: node 0's slot (direct; node 1's slot is strip-conv scratch) or
   // the scratch slot (factored: node 0's slot receives its conv Y)
   if (sp.factored)
-    representation<G>(sm, np, planes, pool + (size_t)(E.S + 1) * node_floats, G::CS, pool);
+    representation<G>(sm, np, planes, pool + (size_t)(E.S + 1) * node_floats, G::CS, pool, ts ? ts + 3 : nullptr);
   else
-    representation<G>(sm, np, planes, pool, G::CS, pool + node_floats);
+    representation<G>(sm, np, planes, pool, G::CS, pool + node_floats, ts ? ts + 3 : nullptr);
+#ifdef MZGO_STAMPS
+  if (ts) ts[0] = __builtin_amdgcn_s_memtime();
+#endif
   if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
   __syncthreads();
+#ifdef MZGO_STAMPS
+  if (ts) ts[1] = __builtin_amdgcn_s_memtime();
+#endif
   if constexpr (G::TREE_CAP > 0) {
     if (sp.num_simulations + 2 <= G::TREE_CAP) {
       sim_loop<G, TreeAcc<G, true>>(sm, np, sp, E, g, TV, key);
@@ -1298,6 +1318,12 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int g = blockIdx.x;
   if (E.status[g] != 0) return;
+#ifdef MZGO_STAMPS
+  unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  tm[0] = __builtin_amdgcn_s_memtime();
+#else
+  unsigned long long* tm = nullptr;
+#endif
   BoardMeta m;
   load_board<G>(sm, E, g, m);
   const int mv = m.moves;
@@ -1315,7 +1341,14 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
   const BoardMeta m0 = m;
   const double* noise = pp.noise ? pp.noise + ((size_t)g * E.max_moves + mv) * G::A : nullptr;
-  run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key);
+#ifdef MZGO_STAMPS
+  tm[1] = __builtin_amdgcn_s_memtime();
+#endif
+  run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
+                tm ? tm + 2 : nullptr);
+#ifdef MZGO_STAMPS
+  tm[4] = __builtin_amdgcn_s_memtime();
+#endif
 
   const TreeView T = TreeViewOf<G>::make(E, g);
   if (wave_id() == 0) {
@@ -1337,6 +1370,22 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   double w = 0.0;
   if (st == BOARD_OK && m.done) w = board_winning<G>(b, pp.komi);
   store_board<G>(sm, E, g, m);
+#ifdef MZGO_STAMPS
+  // move phases (slots 83-87): board load + record, representation, root
+  // priors, the simulations, action choice + board step
+  if (threadIdx.x == 0 && E.stamps) {
+    const unsigned long long t5 = __builtin_amdgcn_s_memtime();
+    unsigned long long* sl = E.stamps + (size_t)blockIdx.x * kStampPhases;
+    sl[83] += tm[1] - tm[0];
+    sl[84] += tm[2] - tm[1];
+    sl[85] += tm[3] - tm[2];
+    sl[86] += tm[4] - tm[3];
+    sl[87] += t5 - tm[4];
+    sl[88] += tm[5] - tm[1];                     // representation: board planes + conv1
+    sl[89] += tm[6] - tm[5];                     //   conv2
+    sl[90] += tm[2] - tm[6];                     //   conv3 + heads
+  }
+#endif
   if (threadIdx.x == 0) {
     E.rec_reward[rec] = w;
     atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);

@@ -53,7 +53,7 @@ def main():
     print(json.dumps({"N": N, "G": G, "S": S, **out}))
 
 
-if __name__ == "__main__" and not os.environ.get("STAMPS"):
+if __name__ == "__main__" and not os.environ.get("STAMPS") and not os.environ.get("MOVE_STAMPS"):
     main()
 
 
@@ -73,7 +73,7 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 88), np.uint64)
+    buf = np.zeros((G, 91), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
@@ -119,3 +119,41 @@ def stamps_report():
 
 if os.environ.get("STAMPS"):
     stamps_report()
+
+
+def move_stamps_report():
+    """With MZGO_LIB=...libmzgo_stamps.so and MOVE_STAMPS=1: cycles per self-play
+    move by phase (k_selfplay_move slots 83-87), averaged over games and moves."""
+    import ctypes
+
+    import numpy as np
+    from mzgo import _lib
+    N = int(os.environ.get("N", 9))
+    G = int(os.environ.get("G", 256))
+    S = int(os.environ.get("S", 200))
+    M = int(os.environ.get("MOVES", 20))
+    C, A = 96, N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda().eval()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    sp = mzgo.SelfPlay(net, G, S)
+    sp.reset()
+    fn = _lib.lib.mzgo_debug_stamps
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
+    buf = np.zeros((G, 91), np.uint64)
+    sp.move()
+    torch.cuda.synchronize()
+    fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))
+    ms = timeit(sp.move, reps=M)
+    fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))
+    per = buf[:, 83:88].astype(np.float64).mean(0) / (M + 1)
+    rep = buf[:, 88:91].astype(np.float64).mean(0) / (M + 1)
+    names = ["board_load_record", "representation", "root_priors_dirichlet", "simulations", "choose_and_step"]
+    tot = per.sum()
+    print(json.dumps({"N": N, "G": G, "S": S, "move_ms": ms,
+                      "cycles_per_move": {n: round(float(v)) for n, v in zip(names, per)},
+                      "share": {n: round(float(v / tot), 3) for n, v in zip(names, per)},
+                      "representation_conv1_conv2_conv3": [round(float(v)) for v in rep]}))
+
+
+if os.environ.get("MOVE_STAMPS"):
+    move_stamps_report()
