@@ -100,7 +100,9 @@ struct HeadPart {
 // lds_in: [CINP][CPAD] staged input.  wpk: packed weights.
 // out: [COUT][out_stride] (global), cells >= out_cells are not stored.
 // NH heads (0..3): head_w[h*COUT + cout]; partial sums land in hp.
-template <class G, int CIN, int COUT, int NH>
+// NGJ: 16-cell tiles per wave job (default the geometry's; conv1 passes 1 so
+// that its (cout group, cell tile) jobs cover every wave).
+template <class G, int CIN, int COUT, int NH, int NGJ = G::NG>
 __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in, const float* __restrict__ wpk,
                                const float* __restrict__ bias, float* __restrict__ out,
                                int out_stride, int out_cells, const float* __restrict__ head_w,
@@ -109,11 +111,14 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
   constexpr int CINP = (CIN + 3) / 4 * 4;
   constexpr int CQ = CINP / 4;                 // k-steps per tap
   constexpr int KS = 9 * CQ;                   // k-steps
-  constexpr int MG = S::MG, MGP = S::MGP, NG = G::NG;
-  constexpr int JOBS = S::NCOG * G::NCG;
-  constexpr int PF = (CQ % 4 == 0) ? 4 : 2;    // A-fragment prefetch ring depth
+  constexpr int MG = S::MG, MGP = S::MGP, NG = NGJ;
+  constexpr int JOBS = S::NCOG * ((G::CT + NG - 1) / NG);
+  // A-fragment prefetch ring depth: the whole weight stream of a job when it
+  // is short (conv1: 18 k-steps -- one memory latency instead of one per
+  // k-step), else 4 or 2 k-steps ahead
+  constexpr int PF = (9 * CQ * S::MGP <= 48) ? 9 * CQ : ((CQ % 4 == 0) ? 4 : 2);
   constexpr int WSTEP = S::NCOG * 64 * MGP;    // floats per k-step in the packed weights
-  static_assert(CQ % PF == 0, "ring depth must divide the k-steps of a tap");
+  static_assert(CQ % PF == 0 || PF == 9 * CQ, "ring depth must divide the k-steps of a tap");
   static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
   typedef typename WFrag<MGP>::T wfrag;
 
@@ -147,8 +152,9 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
     constexpr int WSTEP_F = WSTEP / MGP;  // in wfrag units
     wfrag ring[PF];
 #pragma unroll
-    for (int p = 0; p < PF - 1; ++p) ring[p] = wp[p * WSTEP_F];
+    for (int p = 0; p < (PF == KS ? PF : PF - 1); ++p) ring[p] = wp[p * WSTEP_F];
 
+#pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
       int off[NG];
@@ -165,14 +171,14 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
         const int s = t * CQ + c4;
         // prefetch the weights PF-1 k-steps ahead (a linear stream)
         const int sp = s + PF - 1;
-        if (sp < KS) ring[(c4 + PF - 1) % PF] = wp[sp * WSTEP_F];
+        if (PF < KS && sp < KS) ring[(s + PF - 1) % PF] = wp[sp * WSTEP_F];
         float b[NG];
 #pragma unroll
         for (int ni = 0; ni < NG; ++ni) {
           float v = lrow[(c4 * 4) * G::CPAD + off[ni]];
           b[ni] = ok[ni] ? v : 0.f;
         }
-        const wfrag a = ring[c4 % PF];
+        const wfrag a = ring[s % PF];
 #pragma unroll
         for (int mi = 0; mi < MG; ++mi) {
           const float am = frag_get(a, mi);

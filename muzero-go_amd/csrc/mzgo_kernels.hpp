@@ -185,7 +185,7 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
   __syncthreads();
   HeadPart<G> hp{nullptr};
   const int oc = lat_stride == G::CS ? G::CS : G::CELLS;   // pooled latents also write their 0 pads
-  conv3x3_direct<G, 6, 64, 0>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
+  conv3x3_direct<G, 6, 64, 0, 1>(sm.u.in, np.w_conv1, np.b_conv1, lat, lat_stride, oc, nullptr, hp);
   __syncthreads();
 #ifdef MZGO_STAMPS
   if (ts) ts[0] = __builtin_amdgcn_s_memtime();
