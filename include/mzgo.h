@@ -110,10 +110,10 @@ int mzgo_search(mzgo_engine* eng, const float* root_obs, const double* noise, in
 /* Copy slot g's last search tree to host buffers (synchronises ``stream``):
  * n_nodes; child i32 [n][A]; visits i32 [n]; value_sum f64 [n]; prior f32 [n][A]
  * (row 0 unused); root_prior f64 [A].  Buffers must hold S+1 nodes; NULL skips.
- * After mzgo_search every prior row is final.  After mzgo_selfplay_move the
- * rows of nodes that no select reached may still hold the child's policy
- * logits (priors are formed when a select first reaches a node; the move
- * never reads the others). */
+ * After mzgo_search every row is final.  After mzgo_selfplay_move, the rows
+ * of nodes that no select reached may still hold the child's policy logits
+ * (prior) and stale ids (child): both are formed when a select first reaches
+ * a node (it has no children before), and the move never reads the others. */
 int mzgo_tree_export(mzgo_engine* eng, int g, int32_t* n_nodes_host, int32_t* child_host,
                      int32_t* visits_host, double* value_sum_host, float* prior_host,
                      double* root_prior_host, void* stream);

@@ -329,8 +329,10 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
       float r, v, x[G::AP];
       heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
       policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
-      int* crow = TV.child + (size_t)nid * G::A;
-      for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+      if constexpr (!LAZY) {                 // (a lazy child's row is written when it is settled)
+        int* crow = TV.child + (size_t)nid * G::A;
+        for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+      }
       if (st) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
       if constexpr (LAZY) {
         // the row keeps the logits until a select first reaches the child
@@ -1030,7 +1032,7 @@ __device__ __forceinline__ void settle_all_priors(Smem<G>& sm, const TreeView& T
     for (int n = 1 + wave; n < lim; n += G::WAVES) {
       if (!sm.t.is_raw(n)) continue;
       float q[G::AP];
-      settle_priors<G>(sm.t, TV.prior + (size_t)n * G::A, n, variant, W.fb, W.db, q);
+      settle_priors<G>(sm.t, TV.prior + (size_t)n * G::A, TV.child + (size_t)n * G::A, n, variant, W.fb, W.db, q);
     }
   }
   __syncthreads();

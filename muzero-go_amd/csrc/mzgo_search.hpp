@@ -408,11 +408,16 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::
 }
 
 // A raw prior row (policy logits, see TreeLds::rawp) -> the node's child
-// priors, in place; q gets them too.  One wave; fbuf / dbuf: its LDS scratch.
+// priors, in place; q gets them too.  A raw node has no children yet and its
+// child row was never written: crow gets -1s.  One wave; fbuf / dbuf: its
+// LDS scratch.
 template <class G>
-__device__ __forceinline__ void settle_priors(TreeLds<G>& t, float* row, int node, int variant, float* fbuf,
-                                              double* dbuf, float (&q)[G::AP]) {
+__device__ __forceinline__ void settle_priors(TreeLds<G>& t, float* row, int* crow, int node, int variant,
+                                              float* fbuf, double* dbuf, float (&q)[G::AP]) {
   const int lane = lane_id_local();
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j)
+    if (lane + 64 * j < G::A) crow[lane + 64 * j] = -1;
   float x[G::AP];
 #pragma unroll
   for (int j = 0; j < G::AP; ++j) x[j] = lane + 64 * j < G::A ? row[lane + 64 * j] : 0.f;
@@ -711,12 +716,13 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
           __builtin_amdgcn_s_sleep(1);
       float q[G::AP];
-      settle_priors<G>(t, const_cast<float*>(pr_row), node, sp.variant, t.fbuf, t.dbuf, q);
+      settle_priors<G>(t, const_cast<float*>(pr_row), T.T.child + (size_t)node * G::A, node, sp.variant, t.fbuf,
+                       t.dbuf, q);
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) {
         const int a = lane + 64 * j;
         P[j] = a < G::A ? (double)q[j] : 0.0;
-        ch[j] = a < G::A ? T.T.child[(size_t)node * G::A + a] : -1;
+        ch[j] = -1;
       }
     } else {
 #pragma unroll
