@@ -507,6 +507,7 @@ struct VerifyLds {
   double qx[DMAX][G::A + 1], invr[DMAX][G::A + 1], sq[DMAX][G::A + 1], sx[DMAX][G::A + 1];
   uint64_t elig[DMAX][G::AP];
   double lo_o[DMAX], hi_o[DMAX];    // min / max of q over eligible children other than x
+  double cpx[DMAX];                 // x's c_puct * P
   int x[DMAX], n0[DMAX], N0[DMAX];
   double wpre[DMAX][G::A + 9];      // x_l's value sum after i accepted simulations (+ prefix_sums' tail)
   double wroot[G::A + 9];           // the root's value sum after i
@@ -537,15 +538,23 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   // the node at depth d takes the share v (-1)^(D + 1 - d) of a batch child's backup
   if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
   if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
-  // ---- 1. the levels (one wave each) and the root's own sums ----
-  for (int l = wave; l <= D; l += G::WAVES) {
-    if (l == D) {                                   // the root's value sum after i simulations
+  // ---- 1a. jobs 0..D-1: level l's children (one wave each); jobs D..2D:
+  // the sequential value sums (the root's, then x_l's for each level) on
+  // other waves at the same time ----
+  for (int job = wave; job <= 2 * D; job += G::WAVES) {
+    if (job == D) {                                 // the root's value sum after i simulations
       prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
       continue;
     }
+    if (job > D) {                                  // x_l = p_(l+1), depth l + 1
+      const int l = job - D - 1;
+      prefix_sums<G>(T.ws(T.path(l + 1)), bv, B, alt && ((D - l) & 1), vl.wpre[l]);
+      continue;
+    }
+    const int l = job;
     const int p = T.path(l);
     const int xa = l == 0 ? sm.t.ract : nact[T.path(l + 1)];
-    double lo = INFINITY, hi = -INFINITY, wx = 0.0, cpx = 0.0;
+    double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
     int nx = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
@@ -577,26 +586,29 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
       if (lane == 0) vl.elig[l][j] = el;
       if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
       if (j == (xa >> 6)) {
-        wx = dpp::lane(w, xa & 63);
         nx = __builtin_amdgcn_readlane(n, xa & 63);
         cpx = dpp::lane(cp, xa & 63);
       }
     }
     wave_minmax(lo, hi);
-    if (st) st->lap(75);
-    const int N0 = T.vis(p);
     if (lane == 0) {
       vl.lo_o[l] = lo;
       vl.hi_o[l] = hi;
       vl.x[l] = xa;
       vl.n0[l] = nx;
-      vl.N0[l] = N0;
+      vl.N0[l] = T.vis(p);
+      vl.cpx[l] = cpx;
     }
-    prefix_sums<G>(wx, bv, B, alt && ((D - l) & 1), vl.wpre[l]);   // x_l = p_(l+1): depth l + 1
-    wave_lds_sync();
-    if (st) st->lap(76);
-    // per simulation i (lane i = lane + 64 j): the level as simulation i's
-    // select finds it, and x's score exactly as puct_pick forms it
+    if (st) st->lap(75);
+  }
+  __syncthreads();
+  if (st) st->lap(76);
+  // ---- 1b. per level, per simulation i (lane i = lane + 64 j): the level
+  // as simulation i's select finds it, and x's score exactly as puct_pick
+  // forms it ----
+  for (int l = wave; l < D; l += G::WAVES) {
+    const int nx = vl.n0[l], N0 = vl.N0[l];
+    const double lo = vl.lo_o[l], hi = vl.hi_o[l], cpx = vl.cpx[l];
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
       const int i = lane + 64 * j;
