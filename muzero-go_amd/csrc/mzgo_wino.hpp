@@ -350,6 +350,9 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   f32x4 yp[6];                                // Z [il*3 + ox] in the loop, then Y partial [oy*3 + ox]
 #pragma unroll
   for (int o = 0; o < 6; ++o) yp[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bb[4];                                // this lane's 4 output channels' bias
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bb[r] = active ? bias[m * 16 + kq * 4 + r] : 0.f;
 
   const unsigned long long t_loop = st ? __builtin_amdgcn_s_memtime() : 0ull;
   if (active) {
@@ -455,13 +458,13 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
 #endif
   if (st) { st->wave_add(8 + wave, __builtin_amdgcn_s_memtime() - t_loop); st->lap(6); }
 
-  // epilogue constants before any store (see conv3x3_ring)
-  float bb[4], hw[NH > 0 ? NH : 1][4];
+  // epilogue constants (the bias was loaded before the GEMM, its latency
+  // hidden there)
+  float hw[NH > 0 ? NH : 1][4];
   if (active) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = m * 16 + kq * 4 + r;
-      bb[r] = bias[co];
 #pragma unroll
       for (int hh = 0; hh < NH; ++hh) hw[hh][r] = head_w[hh * COUT + co];
     }
