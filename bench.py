@@ -249,7 +249,7 @@ def main():
                     "equiv_direct_conv_frac_of_fp32_mfma": equiv_tflops / peak_mfma,
                     "dynamics_convs_per_move": convs / max(1.0, moves / world),
                     "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak_mfma,
-                    "note": "latency/LDS-bound (per-game serial chain on one CU); see DESIGN.md section 5",
+                    "note": "not HBM-bound: batched expansions are VALU-bound, parent/representation convs fp32-MFMA-bound, the rest per-game latency; see DESIGN.md section 5",
                     "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a])), "
                                  "batched + replayed expansions"}
         else:
