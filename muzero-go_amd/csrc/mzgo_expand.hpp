@@ -293,7 +293,8 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
 // -> dst [C][CS] (channel-major, pad cells 0), the layout the 3x3 conv reads.
 // Y is cell-major, so 32-channel slabs are transposed through LDS (lds: at
 // least 32 * (CS + 1) floats, free until the conv): coalesced reads and
-// writes.  (One round over all channels at once measured slower.)  All
+// writes; the next slab's loads are in flight during the current slab's
+// transpose.  (One round over all channels at once measured slower.)  All
 // threads; returns synchronised.
 template <class G>
 __device__ __forceinline__ void materialize(float* __restrict__ dst, const float* __restrict__ Ypar,
@@ -302,16 +303,33 @@ __device__ __forceinline__ void materialize(float* __restrict__ dst, const float
   static_assert(G::C % CB == 0, "32-channel slabs");
   const f32x4* Y4 = reinterpret_cast<const f32x4*>(Ypar);
   const f32x4* E4 = reinterpret_cast<const f32x4*>(ea);
-  for (int c0 = 0; c0 < G::C; c0 += CB) {
-    for (int i = threadIdx.x; i < G::CELLS * (CB / 4); i += G::THREADS) {
-      const int p = i / (CB / 4), q = i - p * (CB / 4);
-      const f32x4 y = Y4[p * C4 + c0 / 4 + q], e = E4[region_of<G>(p) * C4 + c0 / 4 + q];
+  // each slab's loads are issued before the previous slab's barrier
+  constexpr int NI = G::CELLS * (CB / 4), R = (NI + G::THREADS - 1) / G::THREADS;
+  f32x4 y[R], e[R];
+  auto load = [&](int c0) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float v = y[k] + e[k];
-        lds[(4 * q + k) * CSP + p] = v > 0.f ? v : 0.f;
+    for (int r = 0; r < R; ++r) {
+      const int i = min((int)threadIdx.x + r * G::THREADS, NI - 1);
+      const int p = i / (CB / 4), q = i - p * (CB / 4);
+      y[r] = Y4[p * C4 + c0 / 4 + q];
+      e[r] = E4[region_of<G>(p) * C4 + c0 / 4 + q];
+    }
+  };
+  load(0);
+  for (int c0 = 0; c0 < G::C; c0 += CB) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = threadIdx.x + r * G::THREADS;
+      if (i < NI) {
+        const int p = i / (CB / 4), q = i - p * (CB / 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float v = y[r][k] + e[r][k];
+          lds[(4 * q + k) * CSP + p] = v > 0.f ? v : 0.f;
+        }
       }
     }
+    if (c0 + CB < G::C) load(c0 + CB);
     __syncthreads();
     for (int i = threadIdx.x; i < CB * G::CS; i += G::THREADS) {
       const int c = i / G::CS, p = i - c * G::CS;
