@@ -71,12 +71,14 @@ def test_batched_search_equals_single_searches():
         assert val1.item() == val_b[i]
 
 
-@pytest.mark.parametrize("N,S,moves", [(5, 40, 6), (6, 128, 10), (9, 200, 20), (19, 300, 60)])
+@pytest.mark.parametrize("N,S,moves", [(5, 40, 6), (6, 128, 10), (9, 200, 20), (9, 600, 12), (19, 300, 60)])
 def test_factored_expansion_equals_direct_conv(N, S, moves):
     """The factored expansion (conv once per parent, children as relu(Y +
     E[a]); mzgo_expand.hpp) against a dynamics conv per simulation, the
     reference's formulation (self_play.py:85-95), on G mid-game roots: the same
-    trees (node for node), child priors and root values up to fp32 rounding."""
+    trees (node for node), child priors and root values up to fp32 rounding.
+    9x9 / 600 simulations runs the HBM-tree variants of the batches and their
+    replay (600 + 2 nodes exceed the LDS tree)."""
     from oracle.positions import random_position
     G = 8
     net = _net(N)
