@@ -1,6 +1,6 @@
 // mzgo_board.hpp -- GymGo board rules as bit-exact integer device code.
 //
-// One workgroup (256 threads) steps one board held in LDS.  Groups are found
+// One workgroup (or one wave of it, BoardWave) steps one board held in LDS.  Groups are found
 // by min-label propagation with pointer jumping (label = smallest cell index
 // of the 4-connected component, as scipy.ndimage.label's components), and
 // liberties are counted as distinct empty neighbour points per group.
@@ -37,6 +37,26 @@ struct BoardLds {
   int* misc;       // [8] 0: nkilled, 1: boxed, 2: ko point, 3/4: area reduction
 };
 
+// Who steps a board: the whole workgroup (the env kernel), or one wave of it
+// (self-play's end of move, where the other waves would only wait at the
+// barriers of the label propagation).
+template <class G>
+struct BoardWG {
+  static constexpr int SIZE = G::THREADS;
+  __device__ static int id() { return threadIdx.x; }
+  __device__ static void sync() { __syncthreads(); }
+  __device__ static bool any(int v) { return __syncthreads_or(v) != 0; }
+  __device__ static bool leader() { return threadIdx.x == 0; }
+};
+template <class G>
+struct BoardWave {
+  static constexpr int SIZE = 64;
+  __device__ static int id() { return lane_id_local(); }
+  __device__ static void sync() { wave_lds_sync(); }
+  __device__ static bool any(int v) { wave_lds_sync(); return __ballot(v != 0) != 0; }
+  __device__ static bool leader() { return lane_id_local() == 0; }
+};
+
 template <class G>
 __device__ __forceinline__ bool nbr(int c, int d, int& n) {
   const int r = c / G::N, col = c - r * G::N;
@@ -50,13 +70,13 @@ __device__ __forceinline__ bool nbr(int c, int d, int& n) {
 
 // label[c] = min cell index of c's 4-connected component of cells whose
 // class(c) is equal; -1 where class(c) == 0.
-template <class G, class ClassFn>
+template <class G, class T, class ClassFn>
 __device__ __forceinline__ void label_components(int* label, ClassFn cls) {
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) label[c] = cls(c) ? c : -1;
-  __syncthreads();
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) label[c] = cls(c) ? c : -1;
+  T::sync();
   for (int it = 0; it < G::CELLS + 2; ++it) {
     int changed = 0;
-    for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+    for (int c = T::id(); c < G::CELLS; c += T::SIZE) {
       const int k = cls(c);
       if (!k) continue;
       int m = label[c];
@@ -69,16 +89,16 @@ __device__ __forceinline__ void label_components(int* label, ClassFn cls) {
       m = j < m ? j : m;
       if (m < label[c]) { label[c] = m; changed = 1; }
     }
-    if (!__syncthreads_or(changed)) break;
+    if (!T::any(changed)) break;
   }
 }
 
 // libs[g] = #distinct empty points adjacent to group g; gsize[g] = #stones
-template <class G>
+template <class G, class T>
 __device__ __forceinline__ void count_liberties(BoardLds<G>& b, bool sizes) {
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) { b.libs[c] = 0; if (sizes) b.gsize[c] = 0; }
-  __syncthreads();
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) { b.libs[c] = 0; if (sizes) b.gsize[c] = 0; }
+  T::sync();
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) {
     if (b.stone[c]) {
       if (sizes) atomicAdd(&b.gsize[b.label[c]], 1);
       continue;
@@ -96,13 +116,13 @@ __device__ __forceinline__ void count_liberties(BoardLds<G>& b, bool sizes) {
       }
     }
   }
-  __syncthreads();
+  T::sync();
 }
 
 // INVD plane for the opponent of ``mover`` (state_utils.compute_invalid_moves)
-template <class G>
+template <class G, class T>
 __device__ __forceinline__ void compute_invalid(BoardLds<G>& b, int mover, int ko) {
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) {
     uint8_t inv;
     if (b.stone[c]) {
       inv = 1;
@@ -122,16 +142,16 @@ __device__ __forceinline__ void compute_invalid(BoardLds<G>& b, int mover, int k
     }
     b.invd[c] = inv;
   }
-  __syncthreads();
-  if (ko >= 0 && threadIdx.x == 0) b.invd[ko] = 1;
-  __syncthreads();
+  T::sync();
+  if (ko >= 0 && T::leader()) b.invd[ko] = 1;
+  T::sync();
 }
 
 enum : int { BOARD_OK = 0, BOARD_ERR_DONE = 1, BOARD_ERR_INVALID = 2, BOARD_ERR_RANGE = 3 };
 
 // gogame.next_state(state, action, canonical=False) on the LDS board.
 // Returns a BOARD_* status (uniform across the workgroup).
-template <class G>
+template <class G, class T = BoardWG<G>>
 __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int action) {
   if (m.done) return BOARD_ERR_DONE;                 // GoEnv.step: assert not self.done
   if (action < 0 || action > G::CELLS) return BOARD_ERR_RANGE;
@@ -140,12 +160,12 @@ __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int acti
   if (action == G::CELLS) {                          // pass
     if (m.passed) m.done = 1;
     m.passed = 1;
-    label_components<G>(b.label, [&](int c) { return (int)b.stone[c]; });
-    count_liberties<G>(b, false);
+    label_components<G, T>(b.label, [&](int c) { return (int)b.stone[c]; });
+    count_liberties<G, T>(b, false);
   } else {
     if (b.invd[action]) return BOARD_ERR_INVALID;    // assert INVD == 0
     m.passed = 0;
-    if (threadIdx.x == 0) {
+    if (T::leader()) {
       b.stone[action] = (int8_t)(player + 1);
       bool boxed = true;
       for (int d = 0; d < 4; ++d) {
@@ -154,11 +174,11 @@ __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int acti
       }
       b.misc[1] = boxed;
     }
-    __syncthreads();
-    label_components<G>(b.label, [&](int c) { return (int)b.stone[c]; });
-    count_liberties<G>(b, true);
+    T::sync();
+    label_components<G, T>(b.label, [&](int c) { return (int)b.stone[c]; });
+    count_liberties<G, T>(b, true);
     // opponent groups adjacent to the new stone with no liberty die
-    if (threadIdx.x == 0) {
+    if (T::leader()) {
       int nk = 0;
       for (int d = 0; d < 4; ++d) {
         int n;
@@ -171,11 +191,11 @@ __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int acti
       b.misc[0] = nk;
       b.misc[2] = (nk == 1 && b.misc[1] && b.gsize[b.killed[0]] == 1) ? b.killed[0] : -1;
     }
-    __syncthreads();
+    T::sync();
     const int nk = b.misc[0];
     ko = b.misc[2];
     if (nk > 0) {
-      for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+      for (int c = T::id(); c < G::CELLS; c += T::SIZE) {
         if (b.stone[c] == 2 - player) {
           const int l = b.label[c];
           bool dead = false;
@@ -183,23 +203,23 @@ __device__ __forceinline__ int board_step(BoardLds<G>& b, BoardMeta& m, int acti
           if (dead) b.stone[c] = 0;
         }
       }
-      __syncthreads();
-      count_liberties<G>(b, false);                   // labels of survivors still hold
+      T::sync();
+      count_liberties<G, T>(b, false);                   // labels of survivors still hold
     }
   }
-  compute_invalid<G>(b, player, ko);
+  compute_invalid<G, T>(b, player, ko);
   m.turn = 1 - m.turn;
   m.moves += 1;
   return BOARD_OK;
 }
 
 // gogame.winning: sign(black_area - white_area - komi), area (Tromp-Taylor).
-template <class G>
+template <class G, class T = BoardWG<G>>
 __device__ __forceinline__ double board_winning(BoardLds<G>& b, double komi) {
-  label_components<G>(b.label, [&](int c) { return b.stone[c] == 0 ? 1 : 0; });
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) { b.libs[c] = 0; b.gsize[c] = 0; }
-  __syncthreads();
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  label_components<G, T>(b.label, [&](int c) { return b.stone[c] == 0 ? 1 : 0; });
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) { b.libs[c] = 0; b.gsize[c] = 0; }
+  T::sync();
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) {
     if (b.stone[c]) continue;
     int f = 0;
 #pragma unroll
@@ -210,9 +230,9 @@ __device__ __forceinline__ double board_winning(BoardLds<G>& b, double komi) {
     if (f) atomicOr(&b.libs[b.label[c]], f);
     atomicAdd(&b.gsize[b.label[c]], 1);
   }
-  __syncthreads();
+  T::sync();
   int black = 0, white = 0;
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = T::id(); c < G::CELLS; c += T::SIZE) {
     if (b.stone[c] == 1) black++;
     else if (b.stone[c] == 2) white++;
     else if (b.label[c] == c) {
@@ -221,13 +241,13 @@ __device__ __forceinline__ double board_winning(BoardLds<G>& b, double komi) {
     }
   }
   // block reduction of (black, white) through LDS
-  if (threadIdx.x == 0) { b.misc[3] = 0; b.misc[4] = 0; }
-  __syncthreads();
+  if (T::leader()) { b.misc[3] = 0; b.misc[4] = 0; }
+  T::sync();
   atomicAdd(&b.misc[3], black);
   atomicAdd(&b.misc[4], white);
-  __syncthreads();
+  T::sync();
   const double diff = (double)b.misc[3] - (double)b.misc[4] - komi;
-  __syncthreads();
+  T::sync();
   return diff > 0 ? 1.0 : (diff < 0 ? -1.0 : 0.0);
 }
 
