@@ -1,6 +1,6 @@
 // mzgo_board.hpp -- GymGo board rules as bit-exact integer device code.
 //
-// One workgroup (or one wave of it, BoardWave) steps one board held in LDS.  Groups are found
+// One workgroup steps one board held in LDS.  Groups are found
 // by min-label propagation with pointer jumping (label = smallest cell index
 // of the 4-connected component, as scipy.ndimage.label's components), and
 // liberties are counted as distinct empty neighbour points per group.
@@ -37,9 +37,9 @@ struct BoardLds {
   int* misc;       // [8] 0: nkilled, 1: boxed, 2: ko point, 3/4: area reduction
 };
 
-// Who steps a board: the whole workgroup (the env kernel), or one wave of it
-// (self-play's end of move, where the other waves would only wait at the
-// barriers of the label propagation).
+// Who steps a board (the board functions' team parameter T): the whole
+// workgroup.  (One wave alone was tried for self-play's end of move: the
+// label propagation ran slower without the other waves' lanes.)
 template <class G>
 struct BoardWG {
   static constexpr int SIZE = G::THREADS;
@@ -48,15 +48,6 @@ struct BoardWG {
   __device__ static bool any(int v) { return __syncthreads_or(v) != 0; }
   __device__ static bool leader() { return threadIdx.x == 0; }
 };
-template <class G>
-struct BoardWave {
-  static constexpr int SIZE = 64;
-  __device__ static int id() { return lane_id_local(); }
-  __device__ static void sync() { wave_lds_sync(); }
-  __device__ static bool any(int v) { wave_lds_sync(); return __ballot(v != 0) != 0; }
-  __device__ static bool leader() { return lane_id_local() == 0; }
-};
-
 template <class G>
 __device__ __forceinline__ bool nbr(int c, int d, int& n) {
   const int r = c / G::N, col = c - r * G::N;

@@ -1378,8 +1378,6 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   }
   __syncthreads();
   const int action = sm.bc[0];
-  // (the whole workgroup steps the board: on wave 0 alone, BoardWave, the
-  // label propagation measured slower)
   BoardLds<G> b = board_lds<G>(sm);
   const int st = board_step<G>(b, m, action);
   __syncthreads();
