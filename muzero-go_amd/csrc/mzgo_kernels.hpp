@@ -992,6 +992,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
                                   const EngineArrays& E, int g, PlaneFn planes, const double* noise,
                                   uint64_t key, unsigned long long* ts = nullptr) {
   const TreeView TV = TreeViewOf<G>::make(E, g);
+  if (threadIdx.x == 0) sm.t.ngrab = 0;             // draw_dirichlet's counter (build_mask's barrier orders it)
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
   float* pool = pool_of<G>(E, g);
   const size_t node_floats = (size_t)G::C * G::CS;
@@ -1004,7 +1005,13 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
 #ifdef MZGO_STAMPS
   if (ts) ts[0] = __builtin_amdgcn_s_memtime();
 #endif
-  if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
+  if (noise) {
+    if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
+  } else {
+    static_assert(G::AP < G::WAVES, "a wave per 64 Gamma draws besides wave 0");
+    draw_dirichlet<G>(sm.t, key, sp.dirichlet_alpha, &sm.t.ngrab);
+    if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key, &sm.t.ngrab);
+  }
   __syncthreads();
 #ifdef MZGO_STAMPS
   if (ts) ts[1] = __builtin_amdgcn_s_memtime();

@@ -428,6 +428,12 @@ __device__ __forceinline__ void settle_priors(TreeLds<G>& t, float* row, int* cr
   if (lane == 0) atomicAnd(&t.rawp[node >> 5], ~(1u << (node & 31)));
 }
 
+// The root's Gamma draws a = lane + 64 (w - 1) on waves w = 1..AP (one per
+// lane, in parallel, while wave 0 forms the softmax): dbuf[a], then *done += 1
+// per wave.  Call from every wave.
+template <class G>
+__device__ __forceinline__ void draw_dirichlet(TreeLds<G>& t, uint64_t key, double alpha, int* done);
+
 // Gamma(alpha) by Marsaglia-Tsang with the alpha+1 boost, from the counter
 // stream (a << 16 | k).  Bounded: at most 64 proposals.
 __device__ __forceinline__ double gamma_draw(uint64_t key, int a, double alpha) {
@@ -447,11 +453,21 @@ __device__ __forceinline__ double gamma_draw(uint64_t key, int a, double alpha) 
   return d * boost;
 }
 
+template <class G>
+__device__ __forceinline__ void draw_dirichlet(TreeLds<G>& t, uint64_t key, double alpha, int* done) {
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  if (w < 1 || w > G::AP) return;
+  const int a = lane_id_local() + 64 * (w - 1);
+  if (a < G::A) t.dbuf[a] = gamma_draw(key, a, alpha);
+  wave_lds_sync();
+  if (lane_id_local() == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Root priors (self_play.py:151-182) into T.root_prior.  noise: injected
 // Dirichlet sample [A] (nullable: sample from the counter stream).  Wave 0.
 template <class G>
 __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
-                                   const double* noise, uint64_t key) {
+                                   const double* noise, uint64_t key, int* drawn = nullptr) {
   const int lane = lane_id_local();
   softmax_wave<G>(t);
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
@@ -460,7 +476,13 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
   if (noise) {
     for (int a = lane; a < G::A; a += 64) t.dbuf[a] = noise[a];
   } else {
-    for (int a = lane; a < G::A; a += 64) t.dbuf[a] = gamma_draw(key, a, sp.dirichlet_alpha);
+    if (drawn) {
+      // the Gamma draws were made by other waves meanwhile (draw_dirichlet)
+      while (__hip_atomic_load(drawn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < G::AP)
+        __builtin_amdgcn_s_sleep(2);
+    } else {
+      for (int a = lane; a < G::A; a += 64) t.dbuf[a] = gamma_draw(key, a, sp.dirichlet_alpha);
+    }
     const double gs = np_pairwise_sum<double, G::A>(t.dbuf);
     for (int a = lane; a < G::A; a += 64) t.dbuf[a] = gs > 0 ? t.dbuf[a] / gs : 1.0 / G::A;
   }
