@@ -76,6 +76,7 @@ struct ExpandLds {
   Wave wv[BATCH ? G::WAVES : 1];          // (after the batch: verify_batch's arrays)
   double bv[BATCH ? G::A + 16 : 1];       // backup value of each batched child (+ tail read by prefix_sums)
   int acts[BATCH ? G::A : 1];             // action of each batched child
+  double bsum[BATCH ? G::A + 16 : 1];     // the root batch's running root sums (prefix_sums)
 };
 
 // board region class of a cell: (row class) * 3 + (column class)

@@ -368,6 +368,34 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
     for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
 }
 
+// dst[0] = w0, dst[k + 1] = dst[k] + (neg ? -v[k] : v[k]) for k < B: the
+// sequential f64 sums (lane 0), 8 at a time without branches, the next 8
+// loads in flight: v is read up to 15 and dst written up to 7 entries past B
+// (those sums are never read).  Wave-level.
+template <class G>
+__device__ __forceinline__ void prefix_sums(double w0, const double* __restrict__ v, int B, bool neg,
+                                            double* __restrict__ dst) {
+  if (lane_id_local() == 0) {
+    double w = w0;
+    dst[0] = w;
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = v[u];
+    for (int k0 = 0; k0 < B; k0 += 8) {
+      double y[8];                                 // the next chunk's loads, in flight during the chain
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[u] = v[k0 + 8 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        w = w + (neg ? -x[u] : x[u]);
+        dst[k0 + u + 1] = w;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = y[u];
+    }
+  }
+}
+
 // Batched root phase.  While the root has unexpanded eligible children,
 // select_leaf (self_play.py:283-287; main.py's select the same) picks one of
 // them by the simulation's draw alone -- no value enters the choice -- so the
@@ -440,10 +468,10 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       }
       if (lane == 0) {
         const bool alt = sp.variant == 0;   // main.py:366-368 does not alternate
-        for (int k = 0; k < K; ++k) {       // the root's sum in simulation order
-          const double v = L.bv[k];
-          T.add(0, alt ? -v : v);
-        }
+        // the root's sum in simulation order: the same f64 additions, the
+        // running sum in a register (prefix_sums' chain) instead of LDS
+        prefix_sums<G>(T.ws(0), L.bv, K, alt, L.bsum);
+        T.set(0, T.vis(0) + K, L.bsum[K]);
         sm.t.newest = -1;                    // every prior row is in HBM already
         sm.t.ycache = 0;                     // L.yc holds the root's Y
       }
@@ -468,34 +496,6 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
 // and first-maximum rule; the batch is accepted up to the first failing i,
 // and the tree takes the accepted simulations' sums.  Returns the number of
 // accepted simulations m >= 1 (all threads; synchronised).
-// dst[0] = w0, dst[k + 1] = dst[k] + (neg ? -v[k] : v[k]) for k < B: the
-// sequential f64 sums (lane 0), 8 at a time without branches, the next 8
-// loads in flight: v is read up to 15 and dst written up to 7 entries past B
-// (those sums are never read).  Wave-level.
-template <class G>
-__device__ __forceinline__ void prefix_sums(double w0, const double* __restrict__ v, int B, bool neg,
-                                            double* __restrict__ dst) {
-  if (lane_id_local() == 0) {
-    double w = w0;
-    dst[0] = w;
-    double x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = v[u];
-    for (int k0 = 0; k0 < B; k0 += 8) {
-      double y[8];                                 // the next chunk's loads, in flight during the chain
-#pragma unroll
-      for (int u = 0; u < 8; ++u) y[u] = v[k0 + 8 + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        w = w + (neg ? -x[u] : x[u]);
-        dst[k0 + u + 1] = w;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = y[u];
-    }
-  }
-}
-
 template <class G, int DMAX>
 struct VerifyLds {
   double cP[DMAX][64 * G::AP];      // c_puct * P as puct_pick forms it
