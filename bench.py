@@ -2,11 +2,12 @@
 
 BASELINE.json's metric on configs[1]: 256 parallel self-play games per GPU,
 200 simulations per move, the reference network (latent_dim 96) with
-deterministic random-init weights, fp32.  One *step* = one self-play move of
-every game on the GPU: one launch of the fused k_selfplay_move kernel
-(observation record, representation + root priors, 200 simulations of
-select / dynamics+prediction (MFMA) / expand / backup, action choice, board
-step).  Games restart (new epoch) every max_moves steps, so any --steps works.
+deterministic random-init weights, fp32.  One *step* = one whole self-play
+epoch: all 256 games from the empty board until
+every one has ended, i.e. N*N = 81 launches of the fused k_selfplay_move
+kernel (each = one move of every unfinished game: observation record,
+representation + root priors, 200 simulations of select / dynamics +
+prediction / expand / backup, action choice, board step).
 
 Multi-GPU (torchrun, one process per GPU): games are sharded by global id
 (rank * G + slot); the only collective is the end-of-run RCCL gather of every
@@ -25,31 +26,6 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "muzero-go_amd")]
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
-
-FLOPS_PER_SIM_9x9 = None  # filled from the geometry below
-
-
-def algorithmic_flops(N, C, S):
-    """Per-simulation and per-move (root) FLOPs of the reference network.
-
-    sim:  dynamics 3x3 conv 2*9*C*C*N^2 + three 1x1 heads 3*2*C*N^2 + embedding add C*N^2
-    root: representation 2*9*N^2*(6*64 + 64*64 + 64*C) + two 1x1 heads 2*2*C*N^2
-    (FCs and softmax are O(A) and omitted.)
-    """
-    cells = N * N
-    sim = 2 * 9 * C * C * cells + 3 * 2 * C * cells + C * cells
-    root = 2 * 9 * cells * (6 * 64 + 64 * 64 + 64 * C) + 2 * 2 * C * cells
-    return sim, root
-
-
-def algorithmic_bytes(N, C, G):
-    """SURVEY.md §8(d)'s algorithmic bytes per simulation (fp32): parent latent
-    read + child latent write 2*C*N^2*4, tree traffic at depth d = 2 (A child
-    priors / ids / visits / value sums, 20 B each, + 12 B backup per level),
-    the new node's priors A*4, and the weights amortised over G games."""
-    A = N * N + 1
-    return 2 * C * N * N * 4 + 2 * A * 20 + 2 * 12 + A * 4 + (9 * C * C + 3 * C + A * C) * 4 // G
-
 
 def mfma_per_conv(N, cin, cout):
     """16x16x4 f32 MFMAs of one 3x3 conv of one board (Winograd at 9x9 / 19x19)."""
@@ -115,11 +91,99 @@ def cpu_baseline_procs(N, C, S, budget_s, procs):
                       f"{budget_s:.0f} s (oracle MCTS + torch-CPU batch-1 net; host has {os.cpu_count()} cpus)"}
 
 
+# MI355X peaks (MI355X_MICROARCH.md): HBM 8 TB/s; fp32 MFMA 157.3 TF/s; VALU
+# issue 2 wave-instructions / clk / CU (4 SIMD-32, a wave64 instruction takes
+# 2 cycles); LDS 128-256 B/clk/CU (the LDS array: one lane group per cycle).
+PEAK_HBM_GBPS = 8000.0
+PEAK_FP32_MFMA_TFLOPS = 157.3
+CUS, PEAK_CLK_GHZ = 256, 2.4
+
+
+def pmc_summary(workload, dynamics):
+    """Per-launch PMC means of k_selfplay_move from rocprofv3 passes of this
+    same bench command (scripts/pmc_selfplay.sh -> profiles/<tag>_pmc.json)."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    if not os.path.exists(path):
+        return None
+    p = json.load(open(path))
+    if p.get("workload") != workload or p.get("dynamics") != dynamics:
+        return None
+    return p
+
+
+def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload):
+    """Roofline of the dominant kernel, k_selfplay_move, per launch.
+
+    Executed MFMA work: the dynamics convs the searches ran (Winograd GEMMs at
+    9x9 / 19x19) + the representation per move.  HBM: the factored algorithm's
+    own bytes (E[a] rows are an L2-resident table and are not charged).  The
+    PMC counters (when profiles/latest_pmc.json is of this workload) give the
+    issue-side units: VALU wave-instructions and LDS-array cycles per launch
+    against their per-CU peaks at the measured clock.  ``bound`` is the unit
+    with the largest fraction."""
+    A, CELLS = N * N + 1, N * N
+    L = counts["launches"]
+    sims_l, moves_l, convs_l = counts["sims"] / L, counts["moves"] / L, counts["convs"] / L
+    ct = (CELLS + 15) // 16
+    mfma_l = 2048 * (convs_l * mfma_per_conv(N, C, C) + moves_l * (
+        9 * 2 * 4 * ct + mfma_per_conv(N, 64, 64) + mfma_per_conv(N, 64, C)))
+    mfma_tf = mfma_l / avg_kern_s / 1e12
+    CS = (CELLS + 15) // 16 * 16
+    if dynamics == "factored":
+        # per simulation the new node's prior (logit) row; per parent conv the
+        # rebuilt latent (written, read) and its Y (written, read); per move the
+        # representation's input and latent and the record
+        hbm_l = (sims_l * A * 4 + convs_l * (2 * C * CS * 4 + 2 * CELLS * C * 4)
+                 + moves_l * ((6 * CELLS + 2 * C * CS) * 4 + 2 * CELLS + A * 8 + 32))
+    else:
+        hbm_l = sims_l * (2 * C * CS * 4 + A * 4) + moves_l * ((6 * CELLS + 2 * C * CS) * 4 + A * 8)
+    units = {
+        "mfma": {"achieved": mfma_tf, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                 "frac": mfma_tf / PEAK_FP32_MFMA_TFLOPS, "per_launch": mfma_l,
+                 "what": "executed v_mfma_f32_16x16x4_f32 FLOPs (parent convs + representation)"},
+        "hbm": {"achieved": hbm_l / avg_kern_s / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                "frac": hbm_l / avg_kern_s / 1e9 / PEAK_HBM_GBPS, "per_launch": hbm_l,
+                "what": "algorithmic HBM bytes of the factored search (E[a] table L2-resident, not charged)"},
+    }
+    pmc = pmc_summary(workload, dynamics)
+    traffic = None
+    if pmc is not None:
+        c = pmc["counters"]
+        dur = pmc["avg_duration_ms"] / 1e3
+        clk = c["GRBM_GUI_ACTIVE"] / 8 / dur / 1e9 if "GRBM_GUI_ACTIVE" in c else PEAK_CLK_GHZ
+        clk = min(clk, PEAK_CLK_GHZ)
+        if "SQ_INSTS_VALU" in c:
+            peak = CUS * 2 * clk * 1e9          # wave-instructions / s
+            ach = c["SQ_INSTS_VALU"] / dur
+            units["valu"] = {"achieved": ach / 1e12, "peak": peak / 1e12, "unit": "Twave-instr/s",
+                             "frac": ach / peak, "per_launch": c["SQ_INSTS_VALU"],
+                             "what": "VALU wave-instructions issued (SQ_INSTS_VALU, MFMA excluded)"}
+        if "SQ_LDS_IDX_ACTIVE" in c:
+            peak = CUS * clk * 1e9              # LDS-array cycles / s
+            ach = c["SQ_LDS_IDX_ACTIVE"] / dur
+            units["lds"] = {"achieved": ach / 1e12, "peak": peak / 1e12, "unit": "Tcycles/s",
+                            "frac": ach / peak, "per_launch": c["SQ_LDS_IDX_ACTIVE"],
+                            "what": "LDS-array busy cycles (SQ_LDS_IDX_ACTIVE) per CU-cycle"}
+        if "hbm_bytes_per_launch" in pmc:
+            traffic = pmc["hbm_bytes_per_launch"]
+        units["pmc_source"] = f"profiles/{pmc['tag']}_pmc.json"
+        units["clock_GHz"] = clk
+    bound = max((k for k in ("mfma", "hbm", "valu", "lds") if k in units), key=lambda k: units[k]["frac"])
+    u = units[bound]
+    return {"bound": bound, "kernel": "k_selfplay_move", "achieved": u["achieved"], "peak": u["peak"],
+            "unit": u["unit"], "frac": u["frac"], "traffic": traffic,
+            "avg_launch_ms": avg_kern_s * 1e3, "sims_per_launch": sims_l,
+            "dynamics_convs_per_move": convs_l / max(moves_l, 1e-9), "units": units,
+            "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a])), batched + "
+                         "replayed expansions" if dynamics == "factored" else
+                         "a Winograd / implicit-GEMM dynamics conv per simulation"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10, help="whole self-play epochs timed")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed epochs")
     ap.add_argument("--board-size", type=int, default=9)
     ap.add_argument("--games", type=int, default=256, help="parallel games per GPU")
     ap.add_argument("--sims", type=int, default=200)
@@ -160,33 +224,37 @@ def main():
     M = sp.max_moves
     stream = torch.cuda.current_stream()
 
-    step_no = 0
+    # One step = one whole self-play epoch: every
+    # slot starts a new game from the empty board and plays until it ends
+    # (double pass, or the N*N move cap).  A finished slot's launches return at
+    # once, so M = N*N launches always finish every game; the epoch index keys
+    # the RNG, so every epoch plays new games.
+    epoch_no = 0
 
-    def one_step():
-        nonlocal step_no
-        if step_no % M == 0:
-            sp.reset(epoch=step_no // M)
-        sp.move()
-        step_no += 1
+    def one_epoch(evs=None):
+        nonlocal epoch_no
+        sp.reset(epoch=epoch_no)
+        for j in range(M):
+            if evs is not None:
+                evs[j][0].record(stream)
+            sp.move()
+            if evs is not None:
+                evs[j][1].record(stream)
+        epoch_no += 1
 
     for _ in range(args.warmup):
-        one_step()
+        one_epoch()
     torch.cuda.synchronize()
     c0 = eng.counters()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(M)]
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if step_no % M == 0:
-            sp.reset(epoch=step_no // M)
-        ev[i][0].record(stream)
-        sp.move()
-        ev[i][1].record(stream)
-        step_no += 1
+        one_epoch(ev[i])
     if world > 1:
         # the trajectory gather of config 3: every rank's packed game records
         # to rank 0's HBM over RCCL (the only collective on the data path)
@@ -197,10 +265,13 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     c1 = eng.counters()
-    sims = c1["simulations"] - c0["simulations"] if c1["simulations"] >= c0["simulations"] else c1["simulations"]
-    moves = c1["moves"] - c0["moves"] if c1["moves"] >= c0["moves"] else c1["moves"]
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+    sims = c1["simulations"] - c0["simulations"]
+    moves = c1["moves"] - c0["moves"]
+    # k_selfplay_move launch durations (HIP events on the launch stream), all
+    # M launches of every timed epoch
+    kern_ms = [a.elapsed_time(b) for e in ev for a, b in e]
+    launches = len(kern_ms)
+    avg_kern_s = sum(kern_ms) / launches / 1e3
 
     if world > 1:
         t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64, device=f"cuda:{local}")
@@ -210,56 +281,10 @@ def main():
         dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
 
     if rank == 0:
-        sim_f, root_f = algorithmic_flops(N, C, S)
-        per_launch_moves = moves / world / args.steps
-        per_launch_sims = sims / world / args.steps
-        launch_flops = per_launch_moves * (S * sim_f + root_f)
-        equiv_tflops = launch_flops / avg_kern_s / 1e12      # the reference formulation's FLOP rate
-        convs = c1["dynamics_convs"] - c0["dynamics_convs"]
-        ct = (N * N + 15) // 16
-        # executed MFMA work: the dynamics convs the searches ran + the
-        # representation (conv1 direct, conv2/conv3 latent convs) per move
-        mfma_launch = 2048 * (convs / args.steps * mfma_per_conv(N, C, C) + per_launch_moves * (
-            9 * 2 * 4 * ct + mfma_per_conv(N, 64, 64) + mfma_per_conv(N, 64, C)))
-        mfma_exec = mfma_launch / avg_kern_s / 1e12
-        peak_mfma = 157.3
-        bytes_sim = algorithmic_bytes(N, C, G)
-        gbps_8d = per_launch_sims * bytes_sim / avg_kern_s / 1e9
-        peak_hbm = 8000.0
-        if args.dynamics == "factored":
-            # The factored algorithm's own HBM bytes: per simulation the child's
-            # E[a] row (9 C f32) and its prior and child-id rows (2 A x 4 B); per
-            # parent conv the rebuilt latent (written, read) and its Y (written,
-            # read into LDS); per move the representation's input and latent and
-            # the record.  (SURVEY §8(d)'s direct-formulation bytes and FLOPs per
-            # simulation are reported beside it: the factored kernel runs past
-            # both of those rooflines because it no longer does that work.)
-            CS = (N * N + 15) // 16 * 16
-            launch_convs = convs / args.steps
-            fact_bytes = (per_launch_sims * (9 * C * 4 + 2 * A * 4)
-                          + launch_convs * (2 * C * CS * 4 + 2 * N * N * C * 4)
-                          + per_launch_moves * ((6 * N * N + 2 * C * CS) * 4 + 2 * N * N + A * 8 + 32))
-            gbps = fact_bytes / avg_kern_s / 1e9
-            roof = {"bound": "hbm", "kernel": "k_selfplay_move", "achieved": gbps, "peak": peak_hbm,
-                    "unit": "GB/s", "frac": gbps / peak_hbm, "traffic": None,
-                    "algorithmic_bytes_per_launch": fact_bytes, "sims_per_launch": per_launch_sims,
-                    "avg_launch_ms": avg_kern_s * 1e3,
-                    "survey_8d_bytes_per_sim": bytes_sim, "equiv_survey_8d_gbps": gbps_8d,
-                    "equiv_direct_conv_tflops": equiv_tflops,
-                    "equiv_direct_conv_frac_of_fp32_mfma": equiv_tflops / peak_mfma,
-                    "dynamics_convs_per_move": convs / max(1.0, moves / world),
-                    "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak_mfma,
-                    "note": "not HBM-bound: batched expansions are VALU-bound, parent/representation convs fp32-MFMA-bound, the rest per-game latency; see DESIGN.md section 5",
-                    "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a])), "
-                                 "batched + replayed expansions"}
-        else:
-            roof = {"bound": "mfma", "kernel": "k_selfplay_move", "achieved": equiv_tflops,
-                    "peak": peak_mfma, "unit": "TFLOP/s", "frac": equiv_tflops / peak_mfma, "traffic": None,
-                    "flops_per_launch": launch_flops, "avg_launch_ms": avg_kern_s * 1e3,
-                    # what the MFMA pipes actually execute (Winograd issues fewer
-                    # MFMA FLOPs than the direct conv's algorithmic count)
-                    "mfma_executed": mfma_exec, "mfma_executed_frac": mfma_exec / peak_mfma,
-                    "algorithm": "winograd F(2,3)xF(3,3)" if N in (9, 19) else "direct implicit GEMM"}
+        workload = f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move"
+        counts = dict(launches=launches, sims=sims / world, moves=moves / world,
+                      convs=(c1["dynamics_convs"] - c0["dynamics_convs"]))
+        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload)
         out = {
             "metric": "MCTS simulations/sec (whole node) + self-play moves/sec, 9x9 Go, 200 sims/move",
             "value": sims / dt,
@@ -274,21 +299,13 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
             "moves_per_s": moves / dt,
-            "config": {"workload": f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move",
+            "config": {"workload": workload, "step": f"one whole self-play epoch: {G} games/GPU from the "
+                                                     f"empty board to their end ({M} launches)",
                        "board_size": N, "latent_dim": C, "games_per_gpu": G, "sims_per_move": S,
                        "parallelism": f"game-sharded x{world}", "compat": "reference",
                        "dynamics": args.dynamics},
             "roofline": roof,
         }
-        prof = os.path.join(ROOT, "profiles", "latest_summary.json")
-        if os.path.exists(prof):
-            p = json.load(open(prof))
-            if (p.get("workload") == out["config"]["workload"] and "k_selfplay_move" in p.get("kernel", "")
-                    and p.get("dynamics", "direct") == args.dynamics):
-                # HBM bytes per launch from rocprofv3 PMC passes of this same command
-                # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/summarize_profile.py)
-                out["roofline"]["traffic"] = p["hbm_bytes_per_launch"]
-                out["roofline"]["traffic_source"] = f"profiles/{p['tag']}_summary.json"
         if cpu_ref is not None:
             out["cpu_baseline"] = cpu_ref
         print(json.dumps(out))

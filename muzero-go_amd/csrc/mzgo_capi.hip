@@ -187,6 +187,7 @@ struct mzgo_engine {
   float* d_w = nullptr;
   size_t d_w_bytes = 0;
   NetParams np{};
+  NetParams* d_np = nullptr;   // device copy of np (k_selfplay_move reads it through a pointer)
   EngineArrays E{};
   int* d_err = nullptr;
   float* d_scr = nullptr;      // initial_inference scratch (strip boards), grown on demand
@@ -269,6 +270,7 @@ struct mzgo_engine {
     np.hs.fc2_w = b + off[14]; np.hs.fc2_b = b + off[15]; np.hs.value_b = b + off[16];
     np.hs.vfc_w = b + off[17]; np.hs.vfc_b = b + off[18]; np.hs.policy_b = b + off[19];
     np.hs.pass_logit = b + off[20];
+    HIPCHK(hipMemcpy(d_np, &np, sizeof np, hipMemcpyHostToDevice));
     dirty = false;
     return MZGO_OK;
   }
@@ -343,6 +345,7 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     // pad cells (>= N*N) of pooled latents are read as zeros and never written
     if (rc == MZGO_OK && hipMemset(E.pool, 0, G * (n1 + 1) * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
       chk(fail(MZGO_EHIP, "hipMemset(pool) failed"));
+    chk(e->alloc(&e->d_np, 1));
     chk(e->alloc(&E.prior, G * n1 * A));
     chk(e->alloc(&E.child, G * n1 * A));
     chk(e->alloc(&E.visits, G * n1));
@@ -534,7 +537,7 @@ int mzgo_selfplay_move(mzgo_engine* e, void* stream) {
   pp.epoch = e->epoch;
   pp.noise = e->noise;
   pp.arena = 0;
-  HIPCHK(e->ks->selfplay_move(e->np, e->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  HIPCHK(e->ks->selfplay_move(e->d_np, e->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
 
@@ -555,7 +558,7 @@ int mzgo_arena_move(mzgo_engine* e, mzgo_engine* opponent, void* stream) {
   pp.epoch = e->epoch;
   pp.noise = e->noise;
   pp.arena = 1;
-  HIPCHK(e->ks->selfplay_move(e->np, opponent->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  HIPCHK(e->ks->selfplay_move(e->d_np, opponent->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
 

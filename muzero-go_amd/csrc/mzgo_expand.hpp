@@ -57,8 +57,10 @@ struct ExpandLds {
   static constexpr int PERW = 3 * G::CS + 9 * G::C + 3 * 64 * G::AP;   // one wave's batch buffers
   static constexpr int PERW_G = G::CS + 9 * G::C;                      // ... with Y streamed from L2
   static_assert(CACHE || 9 * G::C >= 2 * 64 * G::AP, "E's space holds child_priors' scratch (f32 then f64, in turn)");
-  static constexpr bool BATCH = CACHE ? BASE + G::WAVES * PERW + 3 * G::A + 64 <= UF
-                                      : 3 * G::CS + 3 * G::C + G::WAVES * PERW_G + 3 * G::A + 64 <= UF;
+  // tail arrays: bv (A+16 doubles = 2(A+16) floats) and acts (A ints)
+  static constexpr int TAIL = 2 * (G::A + 16) + G::A + 64;
+  static constexpr bool BATCH = CACHE ? BASE + G::WAVES * PERW + TAIL <= UF
+                                      : 3 * G::CS + 3 * G::C + G::WAVES * PERW_G + TAIL <= UF;
   static constexpr bool GLOBAL_Y = BATCH && !CACHE;
   static constexpr int XW = CACHE ? 3 * G::CS : G::CS;   // a wave's head rows; the policy row at PROW
   static constexpr int PROW = CACHE ? 2 * G::CS : 0;
@@ -76,7 +78,6 @@ struct ExpandLds {
   Wave wv[BATCH ? G::WAVES : 1];          // (after the batch: verify_batch's arrays)
   double bv[BATCH ? G::A + 16 : 1];       // backup value of each batched child (+ tail read by prefix_sums)
   int acts[BATCH ? G::A : 1];             // action of each batched child
-  double bsum[BATCH ? G::A + 16 : 1];     // the root batch's running root sums (prefix_sums)
 };
 
 // board region class of a cell: (row class) * 3 + (column class)

@@ -90,6 +90,10 @@ struct Smem {
   int killed[4];
   int misc[8];
   int bc[8];                                             // broadcast slots
+  // a batching configuration's buffers were sized to the union's budget
+  static_assert(!ExpandLds<G, G::CINMAX * G::CPAD>::BATCH ||
+                    sizeof(ExpandLds<G, G::CINMAX * G::CPAD>) <= sizeof(float) * G::CINMAX * G::CPAD,
+                "the batched expansion's LDS must fit the conv staging it overlays");
   __device__ float* heads() { return u.hp; }
   __device__ float* ulds() { return u.in; }             // the union as scratch
   static constexpr int HEAD_PARTS = ConvShape<G::C>::NCOG;
@@ -118,6 +122,10 @@ struct Smem<G, true> {
   int killed[4];
   int misc[8];
   int bc[8];
+  static_assert(!ExpandLds<G, Wino<G>::template v_floats<G::CINMAX>()>::BATCH ||
+                    sizeof(ExpandLds<G, Wino<G>::template v_floats<G::CINMAX>()>) <=
+                        sizeof(float) * Wino<G>::template v_floats<G::CINMAX>(),
+                "the batched expansion's LDS must fit the Winograd input it overlays");
   __device__ float* heads() { return STRIPS ? hfin : u.x.hp; }
   __device__ float* ulds() { return u.v; }              // the union as scratch
   static constexpr int HEAD_PARTS = STRIPS ? 1 : G::C / 16;
@@ -373,11 +381,11 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
 // loads in flight: v is read up to 15 and dst written up to 7 entries past B
 // (those sums are never read).  Wave-level.
 template <class G>
-__device__ __forceinline__ void prefix_sums(double w0, const double* __restrict__ v, int B, bool neg,
-                                            double* __restrict__ dst) {
+__device__ __forceinline__ double prefix_sums(double w0, const double* __restrict__ v, int B, bool neg,
+                                              double* __restrict__ dst) {
+  double w = w0;
   if (lane_id_local() == 0) {
-    double w = w0;
-    dst[0] = w;
+    if (dst) dst[0] = w;
     double x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) x[u] = v[u];
@@ -387,13 +395,14 @@ __device__ __forceinline__ void prefix_sums(double w0, const double* __restrict_
       for (int u = 0; u < 8; ++u) y[u] = v[k0 + 8 + u];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        w = w + (neg ? -x[u] : x[u]);
-        dst[k0 + u + 1] = w;
+        if (k0 + u < B) w = w + (neg ? -x[u] : x[u]);
+        if (dst) dst[k0 + u + 1] = w;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) x[u] = y[u];
     }
   }
+  return w;                                        // lane 0: the sum over all B
 }
 
 // Batched root phase.  While the root has unexpanded eligible children,
@@ -470,8 +479,8 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         const bool alt = sp.variant == 0;   // main.py:366-368 does not alternate
         // the root's sum in simulation order: the same f64 additions, the
         // running sum in a register (prefix_sums' chain) instead of LDS
-        prefix_sums<G>(T.ws(0), L.bv, K, alt, L.bsum);
-        T.set(0, T.vis(0) + K, L.bsum[K]);
+        const double wroot = prefix_sums<G>(T.ws(0), L.bv, K, alt, nullptr);
+        T.set(0, T.vis(0) + K, wroot);
         sm.t.newest = -1;                    // every prior row is in HBM already
         sm.t.ycache = 0;                     // L.yc holds the root's Y
       }
@@ -1332,8 +1341,8 @@ struct PlayParams {
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np_a, NetParams np_b, SearchParams sp,
-                                                             PlayParams pp, EngineArrays E) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(const NetParams* __restrict__ np_a, const NetParams* __restrict__ np_b,
+                                                             SearchParams sp, PlayParams pp, EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
@@ -1350,7 +1359,9 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const int mv = m.moves;
   // arena (main.py:535-549): turn 0 = "current" (np_a), 1 = "best" (np_b); game
   // i starts with turn i % 2 (evaluate, :597-599)
-  const NetParams& np = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? np_b : np_a;
+  // (the parameter blocks live in device memory: a reference chosen between two
+  // by-value kernel arguments would copy both to scratch)
+  const NetParams& np = *((pp.arena && (((pp.game_base + g) + mv) & 1)) ? np_b : np_a);
   const size_t rec = (size_t)g * E.max_moves + mv;
   for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     E.rec_stones[rec * G::CELLS + c] = sm.stone[c];

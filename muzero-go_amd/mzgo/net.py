@@ -6,8 +6,9 @@ Reference: self_play.py:63-128 (RepresentationNetwork, DynamicsNetwork,
 PredictionNetwork, MuZeroNet).  The torch sub-modules below only *hold* the
 parameters so that ``state_dict`` / ``load_state_dict`` / ``.to()`` /
 ``.parameters()`` behave like the reference's; no torch op computes the
-network.  Outputs are inference-only (no autograd graph): the trainer of
-main.py is outside this build's scope.
+network.  Outputs are inference-only (no autograd graph); ``mzgo.trainer``
+(main.py's training step) differentiates through these
+same parameters.
 """
 import torch
 import torch.nn as nn

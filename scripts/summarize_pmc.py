@@ -1,0 +1,67 @@
+"""Summarise a scripts/pmc_selfplay.sh run into profiles/<tag>_pmc.json (and
+profiles/latest_pmc.json, which bench.py reads) + profiles/<tag>_kernel_stats.csv.
+
+Per-launch means over every dispatch of the kernel (the trace's average
+duration; each counter's mean over its pass).  HBM bytes follow
+MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE from separate passes (KB),
+FETCH_SIZE doubled on gfx950, WRITE_SIZE as is.
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import statistics
+import sys
+
+tag = sys.argv[1]
+workload = sys.argv[2] if len(sys.argv) > 2 else "9x9 Go self-play, 256 parallel games/GPU, 200 sims/move"
+dynamics = sys.argv[3] if len(sys.argv) > 3 else "factored"
+kernel = sys.argv[4] if len(sys.argv) > 4 else "k_selfplay_move"
+src = os.path.join("gpurun_out", f"pmc_{tag}")
+os.makedirs("profiles", exist_ok=True)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join("profiles", f"{tag}_kernel_stats.csv"))
+stats = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))) if kernel in r["Name"]][0]
+
+counters = collections.defaultdict(list)
+for d in ("p1", "p2", "fetch", "write"):
+    f = os.path.join(src, d, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    per = collections.defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        if kernel in r["Kernel_Name"]:
+            per[(r["Counter_Name"], r.get("Dispatch_Id", r.get("Correlation_Id", "")))] += float(r["Counter_Value"])
+    for (name, _), v in per.items():
+        counters[name].append(v)
+mean = {k: statistics.mean(v) for k, v in counters.items()}
+out = {
+    "tag": tag, "workload": workload, "dynamics": dynamics,
+    "kernel": stats["Name"], "calls": int(stats["Calls"]),
+    "avg_duration_ms": float(stats["AverageNs"]) / 1e6,
+    "counters": mean, "dispatches_per_counter": {k: len(v) for k, v in counters.items()},
+}
+if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+    out["hbm_bytes_per_launch"] = 2 * mean["FETCH_SIZE"] * 1024 + mean["WRITE_SIZE"] * 1024
+    out["hbm_GBps"] = out["hbm_bytes_per_launch"] / (out["avg_duration_ms"] / 1e3) / 1e9
+c = mean
+dur = out["avg_duration_ms"] / 1e3
+if "GRBM_GUI_ACTIVE" in c:
+    clk = c["GRBM_GUI_ACTIVE"] / 8 / dur
+    cu_cycles = 256 * clk * dur
+    out["derived"] = {
+        "effective_clock_GHz": clk / 1e9,
+        "valu_issue_frac": c.get("SQ_INSTS_VALU", 0) / (2 * cu_cycles),
+        "mfma_busy_frac": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (4 * cu_cycles),
+        "lds_array_busy_frac": c.get("SQ_LDS_IDX_ACTIVE", 0) / cu_cycles,
+        "lds_bank_conflict_share": c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1.0, c.get("SQ_LDS_IDX_ACTIVE", 0)),
+        "wave_wait_any_share": c.get("SQ_WAIT_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
+        "wave_issue_stall_share": c.get("SQ_WAIT_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
+        "wave_active_share": c.get("SQ_ACTIVE_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
+        "note": "fractions of CU-cycles at the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration); "
+                "VALU peak 2 wave-instr/clk/CU, MFMA busy summed over 4 SIMDs, LDS array one cycle/clk/CU; "
+                "wave shares of SQ_WAVE_CYCLES (quad-cycles, as the SQ_WAIT_*/ACTIVE_* counters)",
+    }
+json.dump(out, open(os.path.join("profiles", f"{tag}_pmc.json"), "w"), indent=1)
+json.dump(out, open(os.path.join("profiles", "latest_pmc.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))

@@ -1,0 +1,157 @@
+"""GPU parity at the bench's own kernel configurations.
+
+bench.py times ``k_selfplay_move`` on whole games at 9x9 / 256 games / 200
+simulations (config 2); DESIGN.md also quotes 9x9 / 400 (config 3's per-GPU
+share) and 19x19 / 64 games / 800 (config 4's).  Self-play is the one path
+that leaves lazy rows in the tree (child logits / child ids are formed when a
+select first reaches a node; ``k_search`` settles them, a self-play move does
+not), so its trees are checked here at those sizes, not only through
+``mzgo_search``:
+
+* every game of the batch is replayed on the oracle board
+  (oracle/gogame.py): observations bit-exact, every action legal, the
+  reference's compat-mode policy target (valid mask / sum, self_play.py:378),
+  game length and final reward;
+* the engine counters agree with the records;
+* for a fixed sample of (game, move) roots the device tree left by that move
+  is compared with the oracle's MCTS.run restatement (pinned to the
+  reference's own trees, tests/test_oracle_golden.py) under the same counter
+  streams and injected Dirichlet sample: identical root-child visit counts,
+  root visit count S, root value within 1e-5 (fp32 network).
+
+The sampled-noise run (exactly the bench's code path) is checked for the
+board/record/counter invariants and root visit totals; the injected-noise run
+(same kernel, same sizes; only the Dirichlet source differs) carries the
+tree comparison.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gogame as gg
+from oracle.mcts import root_valid_mask
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1234          # bench.py's seed
+
+
+def _net(N, C=96):
+    import mzgo
+    from oracle.weights import deterministic_state_dict
+    net = mzgo.MuZeroNet(C, N * N + 1).to("cuda").eval()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in deterministic_state_dict(C, N * N + 1, 0).items()})
+    return net
+
+
+def _noise_table(G, M, A):
+    """oracle.rng.injected_noise(SEED, g, mv, A) for every (g, mv), vectorised
+    over the actions (the same u01 draws; each row normalised by its own
+    numpy sum, as injected_noise does)."""
+    from oracle.rng import TAG_DIRICHLET, draw_np, injected_noise, stream_key
+    idx = np.arange(A, dtype=np.uint64) << np.uint64(16)
+    out = np.empty((G, M, A))
+    for g in range(G):
+        for mv in range(M):
+            h = draw_np(stream_key(SEED, g, mv), TAG_DIRICHLET, idx)
+            u = (h >> np.uint64(11)).astype(np.float64) * (2.0 ** -53) + 2.0 ** -20
+            out[g, mv] = u / u.sum()
+    np.testing.assert_array_equal(out[G - 1, M - 1], injected_noise(SEED, G - 1, M - 1, A))
+    return out
+
+
+def _play(net, G, S, check, noise=None):
+    """One epoch of G games from the empty board; returns the histories and
+    the trees (root-child visits, root visits, node count) left by the moves
+    in ``check`` = {move: [games]}."""
+    import mzgo
+    sp = mzgo.SelfPlay(net, G, S, seed=SEED)
+    eng = sp.engine
+    if noise is not None:
+        eng.inject_noise(noise)
+    A = eng.A
+    c0 = eng.counters()                    # net.engine() may hand back a used engine
+    sp.reset(epoch=0)
+    trees = {}
+    for mv in range(sp.max_moves):
+        sp.move()
+        for g in check.get(mv, ()):
+            rec_len = eng.record(g)["length"]
+            if rec_len != mv + 1:          # the game ended before this move
+                continue
+            t = eng.tree(g)
+            rc = t["child"][0]
+            vis = np.array([t["visits"][c] if c >= 0 else 0 for c in rc[:A]], np.int64)
+            trees[(g, mv)] = dict(visits=vis, root_n=int(t["visits"][0]), n=int(t["n"]),
+                                  value=float(t["value_sum"][0] / t["visits"][0]))
+    c1 = eng.counters()
+    c = {k: c1[k] - c0[k] for k in ("simulations", "moves", "games_finished")}
+    c["playing"] = c1["playing"]
+    hists = sp.histories()
+    if noise is not None:
+        eng.inject_noise(None)
+    return hists, trees, c
+
+
+def _replay_all(hists, N, S, counters):
+    assert counters["playing"] == 0 and counters["games_finished"] == len(hists)
+    total = sum(len(h) for h in hists)
+    assert counters["moves"] == total and counters["simulations"] == total * S
+    for h in hists:
+        st = gg.init_state(N)
+        for obs, a, pol, v in zip(h.observations, h.actions, h.policies, h.values):
+            np.testing.assert_array_equal(obs, st)
+            mask = root_valid_mask(obs)
+            assert mask[a] > 0, "illegal action recorded"
+            np.testing.assert_array_equal(pol, mask / mask.sum())
+            assert np.isfinite(v)
+            st = gg.next_state(st, a)
+        ended = bool(gg.game_ended(st))
+        assert len(h) == N * N or ended
+        assert float(h.final_reward) == (float(gg.winning(st)) if ended else 0.0)
+
+
+CONFIGS = [
+    # N, G, S, {move: games} sampled for the oracle tree comparison
+    (9, 256, 200, {0: [0, 131], 7: [5, 200], 20: [17, 255], 41: [3, 64], 66: [99], 80: [128]}),
+    (9, 256, 400, {2: [1], 30: [77], 70: [250]}),
+    (19, 64, 800, {0: [0], 45: [33], 200: [63]}),
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("N,G,S,check", CONFIGS, ids=["9x9_g256_s200", "9x9_g256_s400", "19x19_g64_s800"])
+def test_selfplay_bench_config_matches_oracle(N, G, S, check):
+    from oracle.mcts import MCTS
+    from oracle.net import OracleNet
+    from oracle.rng import SearchHooks
+    from oracle.weights import deterministic_state_dict
+    A, M = N * N + 1, N * N
+    net = _net(N)
+
+    # (1) the bench's exact path: sampled Dirichlet noise
+    hists, trees, c = _play(net, G, S, check)
+    _replay_all(hists, N, S, c)
+    for (g, mv), t in trees.items():
+        assert t["root_n"] == S and int(t["visits"].sum()) == S, (g, mv)
+
+    # (2) injected noise: the trees against the oracle's MCTS.run
+    noise = _noise_table(G, M, A)
+    hists, trees, c = _play(net, G, S, check, noise=noise)
+    _replay_all(hists, N, S, c)
+    assert trees, "no sampled root was still playing"
+    onet = OracleNet(deterministic_state_dict(96, A, 0))
+    for (g, mv), t in sorted(trees.items()):
+        obs = hists[g].observations[mv]
+        hooks = SearchHooks(SEED, g, mv)
+        nz = noise[g, mv]
+        ref = MCTS(onet, A, S, choice=lambda seq, sim, h=hooks: seq[h.choice_index(len(seq), sim)],
+                   noise=lambda p, a, e, nz=nz: (1 - e) * p + e * nz)
+        with torch.no_grad():
+            r_root, _, r_value = ref.run(obs)
+        r_vis = np.array([r_root.children[a]["node"].visit_count if r_root.children[a]["node"] else 0
+                          for a in range(A)])
+        np.testing.assert_array_equal(t["visits"], r_vis, err_msg=f"game {g} move {mv}")
+        assert t["root_n"] == r_root.visit_count == S
+        assert abs(t["value"] - r_value) < 1e-5, (g, mv, t["value"], r_value)
+        assert abs(hists[g].values[mv] - r_value) < 1e-5

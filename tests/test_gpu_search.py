@@ -98,11 +98,14 @@ def test_factored_expansion_equals_direct_conv(N, S, moves):
         np.testing.assert_allclose(a["value_sum"], b["value_sum"], rtol=0, atol=1e-4)
 
 
-def test_sampled_dirichlet_statistics():
+@pytest.mark.parametrize("N", [5, 9, 19])
+def test_sampled_dirichlet_statistics(N):
     """The device Gamma sampler gives Dirichlet(alpha) roots: with epsilon=1
-    the root prior IS the masked, renormalised noise; check its moments."""
-    import mzgo
-    N, S, G = 5, 1, 256
+    the root prior IS the masked, renormalised noise; check its moments.  At
+    9x9 (A=82) and 19x19 (A=362) the draws are split over waves 1..AP
+    (entries a >= 64 come from the other waves), so those entries are
+    checked on their own too (non-stale, same distribution)."""
+    S, G = 1, 256
     A = N * N + 1
     net = _net(N)
     eng = net.engine(num_games=G, num_simulations=S, seed=9, dirichlet_epsilon=1.0,
@@ -111,11 +114,18 @@ def test_sampled_dirichlet_statistics():
     eng.search(obs, move_index=0)
     pri = np.stack([eng.tree(g)["root_prior"] for g in range(G)])
     assert np.allclose(pri.sum(1), 1.0)
+    assert np.all(pri > 0)
     alpha = 0.15
-    mean, var = pri.mean(), pri.var()
     want_var = (1 / A) * (1 - 1 / A) / (A * alpha + 1)
-    assert abs(mean - 1 / A) < 1e-9
-    assert 0.7 * want_var < var < 1.3 * want_var, (var, want_var)
+    assert abs(pri.mean() - 1 / A) < 1e-9
+    parts = [pri] if A <= 64 else [pri, pri[:, 64:]]
+    for part in parts:
+        assert 0.7 * want_var < part.var() < 1.3 * want_var, (part.shape, part.var(), want_var)
+    if A > 64:
+        hi = pri[:, 64:]
+        assert abs(hi.mean() - 1 / A) < 0.1 / A
+        # no two games share a draw (a stale / unwritten entry would repeat)
+        assert len(np.unique(hi)) == hi.size
 
 
 @pytest.mark.parametrize("N,S,moves", [(6, 64, 0), (6, 64, 9), (9, 100, 14), (9, 100, 30)])
