@@ -99,19 +99,21 @@ PEAK_FP32_MFMA_TFLOPS = 157.3
 CUS, PEAK_CLK_GHZ = 256, 2.4
 
 
-def pmc_summary(workload, dynamics):
+def pmc_summary(workload, dynamics, moves_per_launch):
     """Per-launch PMC means of k_selfplay_move from rocprofv3 passes of this
-    same bench command (scripts/pmc_selfplay.sh -> profiles/<tag>_pmc.json)."""
+    same bench command (scripts/pmc_selfplay.sh -> profiles/<tag>_pmc.json);
+    only a profile of the same workload and launch structure counts."""
     path = os.path.join(ROOT, "profiles", "latest_pmc.json")
     if not os.path.exists(path):
         return None
     p = json.load(open(path))
-    if p.get("workload") != workload or p.get("dynamics") != dynamics:
+    if (p.get("workload") != workload or p.get("dynamics") != dynamics
+            or p.get("moves_per_launch", 1) != moves_per_launch):
         return None
     return p
 
 
-def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload):
+def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch):
     """Roofline of the dominant kernel, k_selfplay_move, per launch.
 
     Executed MFMA work: the dynamics convs the searches ran (Winograd GEMMs at
@@ -145,7 +147,7 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload):
                 "frac": hbm_l / avg_kern_s / 1e9 / PEAK_HBM_GBPS, "per_launch": hbm_l,
                 "what": "algorithmic HBM bytes of the factored search (E[a] table L2-resident, not charged)"},
     }
-    pmc = pmc_summary(workload, dynamics)
+    pmc = pmc_summary(workload, dynamics, moves_per_launch)
     traffic = None
     if pmc is not None:
         c = pmc["counters"]
@@ -191,6 +193,8 @@ def main():
     ap.add_argument("--dynamics", choices=["factored", "direct"], default="factored",
                     help="factored: one conv per parent, children as relu(Y + E[a]) (mzgo_expand.hpp); "
                          "direct: a dynamics conv per simulation, as the reference computes it")
+    ap.add_argument("--moves-per-launch", type=int, default=0,
+                    help="moves of every game per k_selfplay_move launch (0 = whole games)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
@@ -226,18 +230,21 @@ def main():
 
     # One step = one whole self-play epoch: every
     # slot starts a new game from the empty board and plays until it ends
-    # (double pass, or the N*N move cap).  A finished slot's launches return at
-    # once, so M = N*N launches always finish every game; the epoch index keys
+    # (double pass, or the N*N move cap).  ``--moves-per-launch`` moves of
+    # every game run in one k_selfplay_move launch (default: the whole game,
+    # so each CU plays its game's moves back to back); the epoch index keys
     # the RNG, so every epoch plays new games.
     epoch_no = 0
+    per = M if args.moves_per_launch <= 0 else args.moves_per_launch
+    chunks = [min(per, M - j) for j in range(0, M, per)]
 
     def one_epoch(evs=None):
         nonlocal epoch_no
         sp.reset(epoch=epoch_no)
-        for j in range(M):
+        for j, k in enumerate(chunks):
             if evs is not None:
                 evs[j][0].record(stream)
-            sp.move()
+            sp.move(k)
             if evs is not None:
                 evs[j][1].record(stream)
         epoch_no += 1
@@ -247,7 +254,7 @@ def main():
     torch.cuda.synchronize()
     c0 = eng.counters()
 
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(M)]
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in chunks]
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -268,7 +275,7 @@ def main():
     sims = c1["simulations"] - c0["simulations"]
     moves = c1["moves"] - c0["moves"]
     # k_selfplay_move launch durations (HIP events on the launch stream), all
-    # M launches of every timed epoch
+    # launches of every timed epoch
     kern_ms = [a.elapsed_time(b) for e in ev for a, b in e]
     launches = len(kern_ms)
     avg_kern_s = sum(kern_ms) / launches / 1e3
@@ -284,7 +291,7 @@ def main():
         workload = f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move"
         counts = dict(launches=launches, sims=sims / world, moves=moves / world,
                       convs=(c1["dynamics_convs"] - c0["dynamics_convs"]))
-        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload)
+        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload, args.moves_per_launch)
         out = {
             "metric": "MCTS simulations/sec (whole node) + self-play moves/sec, 9x9 Go, 200 sims/move",
             "value": sims / dt,
@@ -300,7 +307,8 @@ def main():
             "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
             "moves_per_s": moves / dt,
             "config": {"workload": workload, "step": f"one whole self-play epoch: {G} games/GPU from the "
-                                                     f"empty board to their end ({M} launches)",
+                                                     f"empty board to their end ({len(chunks)} launch(es) "
+                                                     f"of up to {per} moves)",
                        "board_size": N, "latent_dim": C, "games_per_gpu": G, "sims_per_move": S,
                        "parallelism": f"game-sharded x{world}", "compat": "reference",
                        "dynamics": args.dynamics},

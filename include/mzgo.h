@@ -140,6 +140,10 @@ int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uin
  * expansion with direct_dynamics, one per new parent node when factored). */
 int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
+/* Up to ``moves`` consecutive moves of every unfinished slot in ONE launch
+ * (each slot stops at its game's end); the records and RNG streams are those
+ * of ``moves`` mzgo_selfplay_move calls.  moves = max_moves plays whole games. */
+int mzgo_selfplay_moves(mzgo_engine* eng, int moves, void* stream);
 
 /* Arena (main.py:526-611, SelfPlayEvaluator): like mzgo_selfplay_move, but
  * game i (global id) is played between two networks -- eng's ("current",
@@ -149,6 +153,8 @@ int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
  * weights (same board_size and latent_dim).  Replaces the evaluator's
  * MCTS(current/best net).run + argmax loop (main.py:548-568). */
 int mzgo_arena_move(mzgo_engine* eng, mzgo_engine* opponent, void* stream);
+/* ``moves`` arena moves per slot in one launch (as mzgo_selfplay_moves). */
+int mzgo_arena_moves(mzgo_engine* eng, mzgo_engine* opponent, int moves, void* stream);
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
 /* Test hook: use injected Dirichlet samples f64 [G][max_moves][A] (device,
  * caller-owned, must outlive the moves) instead of the counter-RNG sampler;

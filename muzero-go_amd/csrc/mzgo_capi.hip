@@ -525,8 +525,10 @@ int mzgo_selfplay_reset(mzgo_engine* e, int epoch, void* stream) {
   return MZGO_OK;
 }
 
-int mzgo_selfplay_move(mzgo_engine* e, void* stream) {
-  if (!e || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+int mzgo_selfplay_move(mzgo_engine* e, void* stream) { return mzgo_selfplay_moves(e, 1, stream); }
+
+int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
+  if (!e || e->C == 0 || moves < 1) return fail(MZGO_EINVAL, "bad argument");
   int rc = e->sync_weights();
   if (rc) return rc;
   PlayParams pp;
@@ -537,12 +539,17 @@ int mzgo_selfplay_move(mzgo_engine* e, void* stream) {
   pp.epoch = e->epoch;
   pp.noise = e->noise;
   pp.arena = 0;
+  pp.moves = moves;
   HIPCHK(e->ks->selfplay_move(e->d_np, e->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
 
 int mzgo_arena_move(mzgo_engine* e, mzgo_engine* opponent, void* stream) {
-  if (!e || !opponent || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  return mzgo_arena_moves(e, opponent, 1, stream);
+}
+
+int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* stream) {
+  if (!e || !opponent || e->C == 0 || moves < 1) return fail(MZGO_EINVAL, "bad argument");
   if (opponent->N != e->N || opponent->C != e->C)
     return fail(MZGO_EINVAL, "arena engines differ in board size / latent_dim (%d/%d vs %d/%d)", e->N, e->C,
                 opponent->N, opponent->C);
@@ -558,6 +565,7 @@ int mzgo_arena_move(mzgo_engine* e, mzgo_engine* opponent, void* stream) {
   pp.epoch = e->epoch;
   pp.noise = e->noise;
   pp.arena = 1;
+  pp.moves = moves;
   HIPCHK(e->ks->selfplay_move(e->d_np, opponent->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }

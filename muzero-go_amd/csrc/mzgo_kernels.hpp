@@ -1338,6 +1338,7 @@ struct PlayParams {
   const double* noise;    // test hook: injected Dirichlet samples [G][M][A], or null
   int arena;              // 0: one network; 1: main.py's evaluator -- game i's first
                           // mover is network (i % 2), then the networks alternate
+  int moves;              // moves per game in this launch (each game stops at its end)
 };
 
 template <int N, int C>
@@ -1348,14 +1349,18 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int g = blockIdx.x;
   if (E.status[g] != 0) return;
+  BoardMeta m;
+  load_board<G>(sm, E, g, m);
+  // pp.moves moves of this game in one launch (the board stays in LDS between
+  // them): a game's moves run back to back on its CU instead of every move of
+  // every game waiting for the slowest game's move at a launch boundary
+  for (int step = 0; step < pp.moves; ++step) {
 #ifdef MZGO_STAMPS
   unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   tm[0] = __builtin_amdgcn_s_memtime();
 #else
   unsigned long long* tm = nullptr;
 #endif
-  BoardMeta m;
-  load_board<G>(sm, E, g, m);
   const int mv = m.moves;
   // arena (main.py:535-549): turn 0 = "current" (np_a), 1 = "best" (np_b); game
   // i starts with turn i % 2 (evaluate, :597-599)
@@ -1418,6 +1423,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     sl[90] += tm[2] - tm[6];                     //   conv3 + heads
   }
 #endif
+  const bool over = st != BOARD_OK || m.done || m.moves >= E.max_moves;
   if (threadIdx.x == 0) {
     E.rec_reward[rec] = w;
     atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);
@@ -1430,6 +1436,9 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
       E.final_reward[g] = m.done ? w : 0.0;      // env.winner() is 0 unless ended
       atomicAdd(&E.counters[2], 1ull);
     }
+  }
+  if (over) break;
+  __syncthreads();                               // this move's LDS reads before the next move's writes
   }
 }
 

@@ -65,7 +65,9 @@ SIGNATURES = {
     "mzgo_board_set": (_I, [_P, _I, _P, _P, _P, _P]),
     "mzgo_selfplay_reset": (_I, [_P, _I, _P]),
     "mzgo_selfplay_move": (_I, [_P, _P]),
+    "mzgo_selfplay_moves": (_I, [_P, _I, _P]),
     "mzgo_arena_move": (_I, [_P, _P, _P]),
+    "mzgo_arena_moves": (_I, [_P, _P, _I, _P]),
     "mzgo_selfplay_counters": (_I, [_P, _P, _P]),
     "mzgo_selfplay_inject_noise": (_I, [_P, _P]),
     "mzgo_records_export": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

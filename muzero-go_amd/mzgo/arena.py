@@ -49,8 +49,7 @@ class SelfPlayEvaluator:
         eng = self.current.engine(self.num_games, self.S, **self.cfg)
         opp = self.best.engine(self.num_games, self.S, **self.cfg)
         eng.selfplay_reset(self.epoch)
-        for _ in range(self.max_moves):
-            eng.arena_move(opp)
+        eng.arena_move(opp, self.max_moves)          # whole games, one launch
         self.epoch += 1
         N = self.current.board_size
         return np.array([float(history_from_device(eng.record(g), N, self.discount).final_reward)

@@ -194,13 +194,14 @@ class Engine:
     def selfplay_reset(self, epoch=0):
         check(lib.mzgo_selfplay_reset(self._h, epoch, stream_of(self.device)))
 
-    def selfplay_move(self):
-        check(lib.mzgo_selfplay_move(self._h, stream_of(self.device)))
+    def selfplay_move(self, moves=1):
+        """``moves`` moves of every unfinished game in one launch (mzgo_selfplay_moves)."""
+        check(lib.mzgo_selfplay_moves(self._h, int(moves), stream_of(self.device)))
 
-    def arena_move(self, opponent):
-        """One move of every unfinished arena game: this engine's network plays
-        turn 0, ``opponent``'s turn 1 (mzgo_arena_move)."""
-        check(lib.mzgo_arena_move(self._h, opponent.handle, stream_of(self.device)))
+    def arena_move(self, opponent, moves=1):
+        """``moves`` moves of every unfinished arena game in one launch: this
+        engine's network plays turn 0, ``opponent``'s turn 1 (mzgo_arena_moves)."""
+        check(lib.mzgo_arena_moves(self._h, opponent.handle, int(moves), stream_of(self.device)))
 
     def inject_noise(self, noise):
         """Test hook: Dirichlet samples float64 [G, max_moves, A] on the GPU (None = sample)."""

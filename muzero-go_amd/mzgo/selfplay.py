@@ -3,9 +3,10 @@ reference's game-record format.
 
 Reference: ``GameHistory`` (self_play.py:415-450), ``run_self_play_game``
 (:453-526) and ``main``'s pickle writer (:529-596).  Every move of every
-unfinished game is one ``mzgo_selfplay_move`` kernel step on the device:
-observation recorded, MCTS (S simulations), action choice, board step,
-result recorded -- the host only harvests finished records.
+unfinished game is one iteration of the ``k_selfplay_move`` kernel on the
+device: observation recorded, MCTS (S simulations), action choice, board step,
+result recorded; one launch plays any number of moves of every game (whole
+games by default) -- the host only harvests finished records.
 
 CLI (replaces ``python self_play.py``)::
 
@@ -120,15 +121,14 @@ class SelfPlay:
             self.epoch = epoch
         self.engine.selfplay_reset(self.epoch)
 
-    def move(self):
-        """Enqueue one move for every unfinished game (asynchronous)."""
-        self.engine.selfplay_move()
+    def move(self, moves=1):
+        """Enqueue ``moves`` moves for every unfinished game, one launch (asynchronous)."""
+        self.engine.selfplay_move(moves)
 
     def play(self):
-        """Play all G games to the end; returns their GameHistory objects."""
+        """Play all G games to the end (one launch); returns their GameHistory objects."""
         self.reset()
-        for _ in range(self.max_moves):
-            self.move()
+        self.move(self.max_moves)
         if self.engine.counters()["playing"] != 0:
             raise RuntimeError("games still playing after max_moves moves")
         hist = self.histories()

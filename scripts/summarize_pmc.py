@@ -18,6 +18,7 @@ tag = sys.argv[1]
 workload = sys.argv[2] if len(sys.argv) > 2 else "9x9 Go self-play, 256 parallel games/GPU, 200 sims/move"
 dynamics = sys.argv[3] if len(sys.argv) > 3 else "factored"
 kernel = sys.argv[4] if len(sys.argv) > 4 else "k_selfplay_move"
+moves_per_launch = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # bench.py --moves-per-launch (0: whole games)
 src = os.path.join("gpurun_out", f"pmc_{tag}")
 os.makedirs("profiles", exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join("profiles", f"{tag}_kernel_stats.csv"))
@@ -36,7 +37,7 @@ for d in ("p1", "p2", "fetch", "write"):
         counters[name].append(v)
 mean = {k: statistics.mean(v) for k, v in counters.items()}
 out = {
-    "tag": tag, "workload": workload, "dynamics": dynamics,
+    "tag": tag, "workload": workload, "dynamics": dynamics, "moves_per_launch": moves_per_launch,
     "kernel": stats["Name"], "calls": int(stats["Calls"]),
     "avg_duration_ms": float(stats["AverageNs"]) / 1e6,
     "counters": mean, "dispatches_per_counter": {k: len(v) for k, v in counters.items()},

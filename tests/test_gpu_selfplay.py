@@ -161,3 +161,34 @@ def test_sharded_engines_equal_single_engine():
         assert got["final_reward"] == want["final_reward"]
         for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
             assert got[k].tobytes() == want[k].tobytes(), (g, k)
+
+
+@pytest.mark.parametrize("chunks", [[81], [3] * 27, [7, 30, 1, 50]])
+def test_multi_move_launches_equal_single_moves(chunks):
+    """mzgo_selfplay_moves: k moves of every game in one launch (a game stops
+    at its end inside the launch) give the records of k one-move launches,
+    byte for byte -- the RNG streams are keyed by (game, move), not launch."""
+    import mzgo
+    from mzgo import distributed as mdist
+    N, G, S = 9, 32, 40
+    net = _net(N)
+
+    def packed(steps):
+        sp = mzgo.SelfPlay(net, G, S, seed=99)
+        sp.reset()
+        c0 = sp.engine.counters()                # engines are cached per config: counters accumulate
+        for k in steps:
+            sp.move(k)
+        c = sp.engine.counters()
+        assert c["playing"] == 0
+        d = {k: c[k] - c0[k] for k in ("moves", "simulations", "games_finished", "dynamics_convs")}
+        return d, mdist.unpack(mdist.pack_engine(sp.engine).cpu().numpy(), G, sp.max_moves, N)
+
+    c1, want = packed([1] * 81)
+    c2, got = packed(chunks)
+    assert c1 == c2
+    for g in range(G):
+        a, b = mdist.slot_records(got, g), mdist.slot_records(want, g)
+        assert a["length"] == b["length"] and a["final_reward"] == b["final_reward"]
+        for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
+            assert a[k].tobytes() == b[k].tobytes(), (g, k)
