@@ -68,6 +68,12 @@ typedef struct mzgo_config {
                                parent once and expands children as relu(Y + E[a]), exact
                                up to fp32 rounding (see muzero-go_amd/csrc/mzgo_expand.hpp);
                                1 = one dynamics conv per simulation, as the reference does */
+  int tower;                /* 0 = the reference network (self_play.py:63-128); 1 = the
+                               residual-tower network of BASELINE config 5 (mzgo/resnet.py:
+                               conv_in + res_blocks residual blocks in the representation and
+                               the dynamics, the reference's heads), bf16 MFMA with fp32
+                               accumulation, latent_dim a multiple of 64, N in {5, 9, 19} */
+  int res_blocks;           /* residual blocks per tower network (tower = 1) */
 } mzgo_config;
 
 typedef struct mzgo_engine mzgo_engine;

@@ -12,6 +12,7 @@
 
 #include "../../include/mzgo.h"
 #include "mzgo_dispatch.hpp"
+#include "mzgo_tower_host.hpp"
 
 namespace mzgo {
 extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96, kernels_n6_c128,
@@ -50,7 +51,7 @@ namespace {
 
 // Reference state_dict keys (self_play.py:63-128) and their shapes.
 struct Spec {
-  const char* key;
+  std::string key;
   std::vector<int64_t> shape;
 };
 
@@ -196,6 +197,7 @@ struct mzgo_engine {
   int64_t bytes = 0;
   int epoch = 0;
   const double* noise = nullptr;
+  TowerHost* tower = nullptr;   // residual-tower network (mzgo_config.tower, BASELINE config 5)
 
   template <class T>
   int alloc(T** p, size_t n) {
@@ -208,6 +210,12 @@ struct mzgo_engine {
     return MZGO_OK;
   }
   ~mzgo_engine() {
+    if (tower) {
+      for (void* p : {tower->d_wb, (void*)tower->d_wf, (void*)tower->ib, (void*)tower->ob, (void*)tower->s0,
+                      (void*)tower->s1, (void*)tower->shp, (void*)tower->sact})
+        if (p) (void)hipFree(p);
+      delete tower;
+    }
     for (void* p : allocs) (void)hipFree(p);
     if (d_w) (void)hipFree(d_w);
     if (d_scr) (void)hipFree(d_scr);
@@ -218,7 +226,12 @@ struct mzgo_engine {
     if (C == 0) return fail(MZGO_EINVAL, "board-only engine (latent_dim 0) has no network");
     if (!dirty) return MZGO_OK;
     for (const Spec& s : spec)
-      if (!sd.count(s.key)) return fail(MZGO_ENOWEIGHTS, "missing weight '%s'", s.key);
+      if (!sd.count(s.key)) return fail(MZGO_ENOWEIGHTS, "missing weight '%s'", s.key.c_str());
+    if (tower) {
+      HIPCHK(tower->upload(sd, &action_taps));
+      dirty = false;
+      return MZGO_OK;
+    }
     std::vector<std::vector<float>> parts;
     parts.push_back(pack_conv(sd["representation.conv1.weight"].data(), 64, 6, false));
     parts.push_back(sd["representation.conv1.bias"]);
@@ -275,6 +288,24 @@ struct mzgo_engine {
     return MZGO_OK;
   }
 
+  // drop-in inference scratch of the tower engine for B boards (zero borders)
+  int tower_scratch(int B) {
+    TowerHost& t = *tower;
+    if (B <= t.scap) return MZGO_OK;
+    for (void* p : {(void*)t.ib, (void*)t.ob, (void*)t.s0, (void*)t.s1, (void*)t.shp, (void*)t.sact})
+      if (p) HIPCHK(hipFree(p));
+    t.ib = t.ob = t.s0 = t.s1 = nullptr; t.shp = nullptr; t.sact = nullptr; t.scap = 0;
+    const size_t n = (size_t)B * t.slot();
+    for (bf16** q : {&t.ib, &t.ob, &t.s0, &t.s1}) {
+      HIPCHK(hipMalloc((void**)q, n * sizeof(bf16)));
+      HIPCHK(hipMemset(*q, 0, n * sizeof(bf16)));
+    }
+    HIPCHK(hipMalloc((void**)&t.shp, (size_t)B * t.CC * 3 * t.CS * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&t.sact, (size_t)B * sizeof(int)));
+    t.scap = B;
+    return MZGO_OK;
+  }
+
   SearchParams search_params() const {
     SearchParams sp;
     sp.c_puct = cfg.c_puct; sp.discount = cfg.discount;
@@ -314,7 +345,19 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   if (!cfg || !out) return fail(MZGO_EINVAL, "null argument");
   *out = nullptr;
   const int N = cfg->board_size, C = cfg->latent_dim;
-  const KernelSet* ks = find_kernels(N, C == 0 ? 96 : C);
+  const int TW = cfg->tower, RB = cfg->res_blocks;
+  if (TW != 0 && TW != 1) return fail(MZGO_EINVAL, "tower must be 0 (reference network) or 1 (residual tower)");
+  if (TW && RB < 0) return fail(MZGO_EINVAL, "res_blocks must be >= 0");
+  const TowerSet* tset = nullptr;
+  if (TW) {
+    // the residual-tower network (BASELINE config 5): board kernels of the
+    // N x N build, the tower's own conv / tree kernels
+    tset = find_tower(N);
+    if (!tset) return fail(MZGO_EINVAL, "unsupported board_size %d for the tower network (built: 5, 9, 19)", N);
+    if (C < 64 || C % 64 != 0 || C > 1024)
+      return fail(MZGO_EINVAL, "the tower network needs latent_dim a multiple of 64 in [64, 1024], got %d", C);
+  }
+  const KernelSet* ks = find_kernels(N, (C == 0 || TW) ? 96 : C);
   if (!ks) return fail(MZGO_EINVAL, "unsupported board_size %d / latent_dim %d (built: N in {5,6,9,19} with C=96; N=6 with C=128 or 64)", N, C);
   if (cfg->num_games < 1) return fail(MZGO_EINVAL, "num_games must be >= 1");
   if (C != 0 && cfg->num_simulations < 1) return fail(MZGO_EINVAL, "num_simulations must be >= 1");
@@ -332,19 +375,65 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   e->S = C == 0 ? 0 : cfg->num_simulations;
   e->M = cfg->max_moves > 0 ? cfg->max_moves : N * N;
   e->cfg.max_moves = e->M;
-  e->spec = specs(C, e->A);
+  if (TW) {
+    e->spec.clear();
+    for (auto& kv : TowerHost::specs(C, e->A, RB)) e->spec.push_back(Spec{kv.first, kv.second});
+  } else {
+    e->spec = specs(C, e->A);
+  }
   EngineArrays& E = e->E;
   E.S = e->S;
   E.max_moves = e->M;
   const size_t G = e->G, n1 = (size_t)e->S + 1, A = e->A, CELLS = e->CELLS, M = e->M;
   int rc = MZGO_OK;
   auto chk = [&](int r) { if (r != MZGO_OK && rc == MZGO_OK) rc = r; };
-  if (C != 0) {
+  if (C != 0 && !TW) {
     // S+1 node slots + one scratch latent per game
     chk(e->alloc(&E.pool, G * (n1 + 1) * (size_t)C * e->CS));
     // pad cells (>= N*N) of pooled latents are read as zeros and never written
     if (rc == MZGO_OK && hipMemset(E.pool, 0, G * (n1 + 1) * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
       chk(fail(MZGO_EHIP, "hipMemset(pool) failed"));
+  }
+  if (TW) {
+    TowerHost* t = e->tower = new TowerHost();
+    t->ts = tset;
+    t->N = N; t->C = C; t->CC = C / 64; t->blocks = RB; t->G = e->G; t->S = e->S; t->A = e->A;
+    t->P = (N + 2) * (N + 2); t->CS = e->CS;
+    TowerArrays& T = t->TA;
+    T.C = C; T.co_chunks = C / 64;
+    const size_t slot = (size_t)t->slot();
+    // node latents (bf16, zero borders: the conv's padding is never written)
+    chk(e->alloc(&T.pool, G * n1 * slot));
+    chk(e->alloc(&t->t0, G * slot));
+    chk(e->alloc(&t->t1, G * slot));
+    chk(e->alloc(&T.rep_in, G * (size_t)t->P * 64));
+    if (rc == MZGO_OK) {
+      for (auto pr : {std::make_pair((void*)T.pool, G * n1 * slot), std::make_pair((void*)t->t0, G * slot),
+                      std::make_pair((void*)t->t1, G * slot), std::make_pair((void*)T.rep_in, G * (size_t)t->P * 64)})
+        if (hipMemset(pr.first, 0, pr.second * sizeof(bf16)) != hipSuccess) chk(fail(MZGO_EHIP, "hipMemset(tower) failed"));
+    }
+    T.slot = (long long)slot;
+    chk(e->alloc(&T.hpart, G * (size_t)t->CC * 3 * e->CS));
+    chk(e->alloc(&T.rootmask, G * A));
+    chk(e->alloc(&T.passp, G));
+    chk(e->alloc(&T.key, G));
+    chk(e->alloc(&T.playing, G));
+    chk(e->alloc(&T.evalact, G));
+    chk(e->alloc(&T.in_idx, G));
+    chk(e->alloc(&T.out_idx, G));
+    chk(e->alloc(&T.root_idx, G));
+    chk(e->alloc(&T.act, G));
+    chk(e->alloc(&T.job, G * 3));
+    chk(e->alloc(&T.simc, G));
+    if (rc == MZGO_OK) {
+      std::vector<int> ri(G);
+      for (size_t g = 0; g < G; ++g) ri[g] = (int)(g * n1);
+      if (hipMemcpy(T.root_idx, ri.data(), G * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemset(T.playing, 0, G * sizeof(int)) != hipSuccess || hipMemset(T.evalact, 0, G * sizeof(int)) != hipSuccess)
+        chk(fail(MZGO_EHIP, "tower index setup failed"));
+    }
+  }
+  if (C != 0) {
     chk(e->alloc(&e->d_np, 1));
     chk(e->alloc(&E.prior, G * n1 * A));
     chk(e->alloc(&E.child, G * n1 * A));
@@ -394,7 +483,7 @@ int64_t mzgo_engine_device_bytes(const mzgo_engine* e) { return e ? e->bytes + (
 int mzgo_set_weights(mzgo_engine* e, const char* key, const float* data, const int64_t* shape, int ndim) {
   if (!e || !key || !data || (!shape && ndim > 0)) return fail(MZGO_EINVAL, "null argument");
   for (const Spec& s : e->spec) {
-    if (std::strcmp(s.key, key) != 0) continue;
+    if (s.key != key) continue;
     if ((int)s.shape.size() != ndim) return fail(MZGO_EINVAL, "'%s': expected %zu dims, got %d", key, s.shape.size(), ndim);
     size_t n = 1;
     for (int i = 0; i < ndim; ++i) {
@@ -421,6 +510,18 @@ int mzgo_initial_inference(mzgo_engine* e, const float* obs, int B, float* laten
   if (!e || !obs || !latent || !value || !logits || B < 1) return fail(MZGO_EINVAL, "bad argument");
   int rc = e->sync_weights();
   if (rc) return rc;
+  if (e->tower) {
+    if ((rc = e->tower_scratch(B))) return rc;
+    TowerHost& t = *e->tower;
+    hipStream_t s = (hipStream_t)stream;
+    TowerArrays Tb = t.TA;
+    Tb.hpart = t.shp;
+    HIPCHK(t.ts->tin(obs, t.ib, B, t.C, 1, t.slot(), s));
+    HIPCHK(t.tower(t.rep, t.ib, nullptr, t.slot(), t.ob, nullptr, t.slot(), nullptr, nullptr, B, t.s0, t.s1, t.shp, s));
+    HIPCHK(t.ts->tout(t.ob, latent, B, t.C, s));
+    HIPCHK(t.ts->theads(Tb, B, 0, nullptr, value, logits, s));
+    return MZGO_OK;
+  }
   float* scr = nullptr;
   if (e->ks->rep_scratch) {
     const size_t need = (size_t)B * e->ks->rep_scratch;
@@ -443,6 +544,19 @@ int mzgo_recurrent_inference(mzgo_engine* e, const float* latent, const int64_t*
     return fail(MZGO_EINVAL, "bad argument");
   int rc = e->sync_weights();
   if (rc) return rc;
+  if (e->tower) {
+    if ((rc = e->tower_scratch(B))) return rc;
+    TowerHost& t = *e->tower;
+    hipStream_t s = (hipStream_t)stream;
+    TowerArrays Tb = t.TA;
+    Tb.hpart = t.shp;
+    HIPCHK(launch_tact(action, t.sact, B, e->A, e->d_err, s));
+    HIPCHK(t.ts->tin(latent, t.ib, B, t.C, 0, t.slot(), s));
+    HIPCHK(t.tower(t.dyn, t.ib, nullptr, t.slot(), t.ob, nullptr, t.slot(), t.sact, nullptr, B, t.s0, t.s1, t.shp, s));
+    HIPCHK(t.ts->tout(t.ob, next_latent, B, t.C, s));
+    HIPCHK(t.ts->theads(Tb, B, 1, reward, value, logits, s));
+    return MZGO_OK;
+  }
   HIPCHK(e->ks->recurrent_inference(e->np, latent, action, B, next_latent, reward, value, logits,
                                     e->d_err, (hipStream_t)stream));
   return MZGO_OK;
@@ -465,6 +579,17 @@ int mzgo_search(mzgo_engine* e, const float* root_obs, const double* noise, int 
   if (!e || !root_obs || G < 1 || G > e->G) return fail(MZGO_EINVAL, "bad argument (G=%d, engine has %d slots)", G, e ? e->G : 0);
   int rc = e->sync_weights();
   if (rc) return rc;
+  if (e->tower) {
+    TowerHost& t = *e->tower;
+    hipStream_t s = (hipStream_t)stream;
+    const SearchParams sp = e->search_params();
+    HIPCHK(hipMemsetAsync(t.TA.playing, 0, e->G * sizeof(int), s));
+    HIPCHK(t.ts->obs_search(t.TA, sp, root_obs, e->cfg.game_base, move_index, G, s));
+    HIPCHK(t.root_phase(sp, e->E, noise, e->A, 0, s));
+    HIPCHK(t.simulations(sp, e->E, s));
+    HIPCHK(t.ts->search_out(e->E, G, visits, value, s));
+    return MZGO_OK;
+  }
   HIPCHK(e->ks->search(e->np, e->search_params(), e->E, root_obs, noise, G, e->cfg.game_base, move_index,
                        visits, value, (hipStream_t)stream));
   return MZGO_OK;
@@ -540,6 +665,20 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
   pp.noise = e->noise;
   pp.arena = 0;
   pp.moves = moves;
+  if (e->tower) {
+    // one move of every game: observation + representation tower + root,
+    // S x (select, dynamics tower, expand), action choice + board step
+    TowerHost& t = *e->tower;
+    hipStream_t s = (hipStream_t)stream;
+    const SearchParams sp = e->search_params();
+    for (int k = 0; k < moves; ++k) {
+      HIPCHK(t.ts->obs(t.TA, sp, pp, e->E, e->G, s));
+      HIPCHK(t.root_phase(sp, e->E, e->noise, (long long)e->M * e->A, 1, s));
+      HIPCHK(t.simulations(sp, e->E, s));
+      HIPCHK(t.ts->choose(t.TA, sp, pp, e->E, e->G, s));
+    }
+    return MZGO_OK;
+  }
   HIPCHK(e->ks->selfplay_move(e->d_np, e->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
@@ -550,6 +689,7 @@ int mzgo_arena_move(mzgo_engine* e, mzgo_engine* opponent, void* stream) {
 
 int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* stream) {
   if (!e || !opponent || e->C == 0 || moves < 1) return fail(MZGO_EINVAL, "bad argument");
+  if (e->tower || opponent->tower) return fail(MZGO_EINVAL, "the arena runs the reference network only (tower 0)");
   if (opponent->N != e->N || opponent->C != e->C)
     return fail(MZGO_EINVAL, "arena engines differ in board size / latent_dim (%d/%d vs %d/%d)", e->N, e->C,
                 opponent->N, opponent->C);

@@ -1,0 +1,632 @@
+// mzgo_tower.hpp -- BASELINE config 5: MuZero with 20-block residual networks
+// at 19x19 / 1600 simulations (no reference
+// counterpart -- the architecture is mzgo/resnet.py's torch module, which is
+// also the parity reference).
+//
+// The reference's dynamics is ONE conv (self_play.py:85-95), so the main
+// engine can factor it (mzgo_expand.hpp); a residual tower is nonlinear after
+// its first conv, so every simulation needs the whole tower on its leaf.  The
+// per-game-per-CU megakernel cannot feed the MFMA pipes with 41 C=256 convs
+// per simulation, so this engine splits the search from the evaluation:
+//
+//   k_tselect   one wave per game: select_leaf (self_play.py:239-335) on the
+//               game's HBM tree -> (leaf latent slot, action, new node slot)
+//   k_tconv     x 41: the tower, ALL games' leaves in one launch per conv --
+//               implicit GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32
+//               accumulate), one (board, 64-cout chunk) per workgroup
+//   k_texpand   one wave per game: heads -> child priors, backup (:198-230)
+//
+// Each game contributes exactly one leaf per simulation step, so the batch
+// keeps every game's sequential semantics (no virtual loss).
+//
+// Activations (bf16) are stored per board as [C/64 chunks][P][64], P = (N+2)^2
+// padded pixels with a zero border (the conv's zero padding, never written),
+// each pixel's 128-byte row of 64 channels in 8 pieces of 16 bytes, piece j
+// at position j ^ ((q >> 1) & 7) (q = padded pixel index): the LDS image of a
+// chunk is a straight copy (global_load_lds) and the A-fragment reads of 16
+// consecutive pixels are bank-conflict free.  Weights are packed the same way
+// per (cout chunk, cin chunk, tap): [64 cout rows][64 cin], piece swizzled by
+// row.
+#pragma once
+#include "mzgo_kernels.hpp"
+
+namespace mzgo {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int N_>
+struct TGeo {
+  static constexpr int N = N_;
+  static constexpr int CELLS = N * N;
+  static constexpr int A = CELLS + 1;
+  static constexpr int AP = (A + 63) / 64;
+  static constexpr int CS = (CELLS + 15) / 16 * 16;     // head-partial row stride
+  static constexpr int W = N + 2;                       // padded board side
+  static constexpr int P = W * W;                       // padded pixels
+  static constexpr int PB = (P * 128 + 4095) / 4096 * 4096;   // LDS bytes of one 64-channel chunk
+  static constexpr int NPW = PB / 4096;                 // 1-KiB DMA pieces per wave per chunk
+  static constexpr int PST = NPW / 2;                   // steps over which the next chunk is fetched
+  static constexpr int TT = (CELLS + 15) / 16;          // 16-pixel M tiles of a board
+  static constexpr int MT = (TT + 3) / 4;               // tiles per wave (4 waves)
+  static constexpr int WSLOT = 64 * 64 * 2;             // one (tap, cin chunk) weight tile
+  static constexpr int LDS = 2 * PB + 3 * WSLOT + 4 * 64 * 4;
+  // tree kernels: one wave per game
+  static constexpr int THREADS = 64, WAVES = 1, TREE_CAP = 0;
+  static_assert(PST <= 7, "a chunk's DMA must be issued within taps 0..6");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(2 * PB >= CELLS * 272, "epilogue staging must fit the patch buffers");
+};
+
+// element offset of (padded pixel q, channel c) inside one 64-channel chunk
+__device__ __forceinline__ int tpix(int q, int piece) { return q * 64 + ((piece ^ ((q >> 1) & 7)) << 3); }
+
+// ---------------------------------------------------------------------------
+// One 3x3 conv (+ bias [+ E-table term] [+ residual], ReLU) for nboards
+// boards: out[b] = relu(conv(in[b]) + bias + E[act[b]][region] + res[b]).
+// Optional fused 1x1 heads: hpart[b][cout chunk][h][cell] = sum over the
+// chunk's 64 channels of headw[h][c] * out (the bf16-rounded output).
+// ---------------------------------------------------------------------------
+struct TConvArgs {
+  const bf16* in; const int* in_idx; long long in_stride;       // board b: in + idx(b) * stride
+  bf16* out; const int* out_idx; long long out_stride;
+  const bf16* res; const int* res_idx; long long res_stride;    // nullable
+  const bf16* w;                                                // [co][ci][9][64][64] packed
+  const float* bias;                                            // [CO]
+  const float* etab; const int* act;                            // nullable: E [A][9][CO], act[b]
+  const float* headw; float* hpart;                             // nullable: [3][CO], [b][co][3][CS]
+  const int* active;                                            // nullable: board b skipped if 0
+  int nboards, ci_chunks, co_chunks;
+};
+
+template <class G, int T>
+struct TapOff { static constexpr int v = (T / 3) * G::W + (T % 3); };
+
+// s_waitcnt vmcnt for step (cc, t): the DMAs younger than weight tile W(s)
+// are the next chunk's pieces of steps s-2 and s-1 and W(s+1) (see k_tconv).
+template <class G, int T>
+__device__ __forceinline__ void tconv_wait(bool nextp, bool last) {
+  constexpr int p2 = (T >= 2 && T - 2 < G::PST) ? 2 : 0;
+  constexpr int p1 = (T >= 1 && T - 1 < G::PST) ? 2 : 0;
+  const int w1 = (last && T == 8) ? 0 : 2;
+  if (nextp) {
+    if (w1) wait_vmcnt<p2 + p1 + 2>(); else wait_vmcnt<p2 + p1>();
+  } else {
+    if (w1) wait_vmcnt<2>(); else wait_vmcnt<0>();
+  }
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
+  typedef TGeo<N> G;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
+  const int CO = a.co_chunks, CC = a.ci_chunks;
+  // block -> (board, cout chunk); a board's chunks on one XCD (blocks b, b+8,
+  // ... share one under round-robin dispatch: speed only) when the grid allows
+  const int bid = blockIdx.x;
+  int b, cg;
+  if (a.nboards % 8 == 0) {
+    const int x = bid & 7, k = bid >> 3;
+    b = x + 8 * (k / CO);
+    cg = k % CO;
+  } else {
+    b = bid / CO;
+    cg = bid % CO;
+  }
+  if (a.active && !a.active[b]) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* const patch0 = lds;
+  char* const wring = lds + 2 * G::PB;
+  float* const sbias = reinterpret_cast<float*>(lds + 2 * G::PB + 3 * G::WSLOT);
+  float* const shw = sbias + 64;
+  const bf16* in = a.in + (long long)(a.in_idx ? a.in_idx[b] : b) * a.in_stride;
+  const bf16* wsrc = a.w + (size_t)cg * CC * 9 * 64 * 64;
+  if (tid < 64) {
+    sbias[tid] = a.bias[cg * 64 + tid];
+    if (a.headw)
+      for (int h = 0; h < 3; ++h) shw[h * 64 + tid] = a.headw[h * CO * 64 + cg * 64 + tid];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA counts below start from zero
+
+  // DMA issue helpers (16 B per lane; the LDS destination is base + lane*16)
+  auto issue_patch_pieces = [&](int cc, int buf, int k0, int k1) {
+    const char* src = reinterpret_cast<const char*>(in + (size_t)cc * G::P * 64);
+    for (int k = k0; k < k1; ++k) {
+      const int ii = k * 4 + wave;                       // 1-KiB piece of the chunk
+      const int piece = ii * 64 + lane;                  // 16-B piece
+      const char* g = src + (piece * 16 < G::P * 128 ? piece * 16 : 0);
+      dma16(g, lds_addr(patch0 + buf * G::PB + ii * 1024));
+    }
+  };
+  auto issue_w = [&](int s) {
+    const char* src = reinterpret_cast<const char*>(wsrc + (size_t)s * 64 * 64);
+    char* slot = wring + (s % 3) * G::WSLOT;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int ii = k * 4 + wave;
+      dma16(src + ii * 1024 + lane * 16, lds_addr(slot + ii * 1024));
+    }
+  };
+  const int total = 9 * CC;
+  issue_patch_pieces(0, 0, 0, G::NPW);
+  issue_w(0);
+  if (total > 1) issue_w(1);
+
+  // per-lane A-fragment pixel bases (pixel p = tile*16 + (lane & 15))
+  int qb[G::MT];
+#pragma unroll
+  for (int i = 0; i < G::MT; ++i) {
+    const int p = (wave * G::MT + i) * 16 + (lane & 15);
+    qb[i] = p < G::CELLS ? (p / N) * G::W + (p % N) : 0;
+  }
+  // per-lane B-fragment byte offsets (cout row n*16 + (lane & 15), piece lane >> 4)
+  int boff[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int r = n * 16 + (lane & 15);
+    boff[n] = r * 128 + (((lane >> 4) ^ ((r >> 1) & 7)) << 4);
+  }
+  f32x4 acc[G::MT][4];
+#pragma unroll
+  for (int i = 0; i < G::MT; ++i)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int cc = 0; cc < CC; ++cc) {
+    const bool nextp = cc + 1 < CC, last = !nextp;
+    const char* pbuf = patch0 + (cc & 1) * G::PB;
+    auto step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const int s = cc * 9 + t;
+      tconv_wait<G, t>(nextp, last);
+      lds_barrier();                                   // W(s) (and chunk cc) landed for every wave
+      if (s + 2 < total) issue_w(s + 2);
+      if (nextp && t < G::PST) issue_patch_pieces(cc + 1, (cc + 1) & 1, 2 * t, 2 * t + 2);
+      const char* ws = wring + (t % 3) * G::WSLOT;
+      bf16x8 bf[4][2];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        bf[n][0] = *reinterpret_cast<const bf16x8*>(ws + boff[n]);
+        bf[n][1] = *reinterpret_cast<const bf16x8*>(ws + (boff[n] ^ 64));
+      }
+#pragma unroll
+      for (int i = 0; i < G::MT; ++i) {
+        if (wave * G::MT + i >= G::TT) break;          // wave-uniform
+        const int q = qb[i] + TapOff<G, t>::v;
+        const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(pbuf + off);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(pbuf + (off ^ 64));
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[n][0], acc[i][n], 0, 0, 0);
+          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[n][1], acc[i][n], 0, 0, 0);
+        }
+      }
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{});
+    step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
+  }
+  lds_barrier();                                       // every wave's last reads done
+
+  // epilogue 1: accumulators -> fp32 staging [cell][68] (over the patch buffers)
+  float* st = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < G::MT; ++i) {
+    const int ti = wave * G::MT + i;
+    if (ti >= G::TT) break;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = ti * 16 + (lane >> 4) * 4 + r;
+        if (p < G::CELLS) st[p * 68 + n * 16 + (lane & 15)] = acc[i][n][r];
+      }
+  }
+  __syncthreads();
+  // epilogue 2: 8 channels per thread: bias, E term, residual, ReLU, bf16 store, head partials
+  bf16* out = a.out + (long long)(a.out_idx ? a.out_idx[b] : b) * a.out_stride + (size_t)cg * G::P * 64;
+  const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
+                          : nullptr;
+  const float* et = a.etab ? a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64 : nullptr;
+  for (int idx = tid; idx < G::CELLS * 8; idx += 256) {
+    const int p = idx >> 3, j = idx & 7;
+    const int y = p / N, x = p - y * N;
+    const int q = (y + 1) * G::W + (x + 1);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(st + p * 68 + j * 8);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(st + p * 68 + j * 8 + 4);
+    float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += sbias[j * 8 + k];
+    if (et) {
+      const int reg = 3 * (y == 0 ? 0 : (y == N - 1 ? 2 : 1)) + (x == 0 ? 0 : (x == N - 1 ? 2 : 1));
+      const f32x4 e0 = *reinterpret_cast<const f32x4*>(et + (size_t)reg * CO * 64 + j * 8);
+      const f32x4 e1 = *reinterpret_cast<const f32x4*>(et + (size_t)reg * CO * 64 + j * 8 + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[k] += e0[k]; v[k + 4] += e1[k]; }
+    }
+    const int off = tpix(q, j);
+    if (res) {
+      const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(res + off);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += (float)r8[k];
+    }
+    bf16x8 o8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o8[k] = (bf16)(v[k] > 0.f ? v[k] : 0.f);
+    *reinterpret_cast<bf16x8*>(out + off) = o8;
+    if (a.headw) {
+      float h[3];
+#pragma unroll
+      for (int hh = 0; hh < 3; ++hh) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += shw[hh * 64 + j * 8 + k] * (float)o8[k];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        h[hh] = s;
+      }
+      if (j == 0) {
+        float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
+        hp[0] = h[0];
+        hp[G::CS] = h[1];
+        hp[2 * G::CS] = h[2];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-game tree kernels (one wave per game; the tree is in HBM between
+// launches, exactly the arrays of the main engine's EngineArrays).
+// ---------------------------------------------------------------------------
+struct TowerArrays {
+  bf16* pool;            // [G*(S+1)] node latents (slot g*(S+1) + node)
+  long long slot;        // elements per latent slot: (C/64) * P * 64
+  bf16* rep_in;          // [G][P*64] representation input (6 planes, 64-channel chunk)
+  float* hpart;          // [G][C/64][3][CS] fused head partials
+  uint8_t* rootmask;     // [G][A] valid_board (INVD == 0), 1 for pass
+  double* passp;         // [G] pass prior
+  uint64_t* key;         // [G] RNG stream key of the current search
+  int* playing;          // [G] representation / root / choose run for this slot
+  int* evalact;          // [G] this simulation step evaluates a leaf
+  int* in_idx;           // [G] latent slot of the leaf being expanded
+  int* out_idx;          // [G] latent slot of the new node
+  int* root_idx;         // [G] g*(S+1)
+  int* act;              // [G] action applied to the leaf
+  int* job;              // [G][3] leaf, depth, new node id
+  int* simc;             // [G] simulation index
+  int C, co_chunks;
+  HeadScalars hs;
+  const float* headw;    // [3][C]: reward_conv, value_conv, policy_conv
+};
+
+template <class G>
+__device__ __forceinline__ void tload_mask(TreeLds<G>& t, const TowerArrays& T, int g) {
+  for (int a = threadIdx.x; a < G::A; a += 64) t.valid[a] = T.rootmask[(size_t)g * G::A + a];
+  if (threadIdx.x == 0) t.pass_prior = T.passp[g];
+  t.newest = -1;
+  t.newp_node = -1;
+  t.rowc_node = -1;
+  wave_lds_sync();
+}
+
+// sum of a board's head partials over the cout chunks (ascending) -> hp [3][CS]
+template <class G>
+__device__ __forceinline__ void tsum_heads(const TowerArrays& T, int b, float* hp) {
+  const float* src = T.hpart + (size_t)b * T.co_chunks * 3 * G::CS;
+  for (int i = threadIdx.x; i < 3 * G::CS; i += 64) {
+    float s = src[i];
+    for (int c = 1; c < T.co_chunks; ++c) s += src[(size_t)c * 3 * G::CS + i];
+    hp[i] = s;
+  }
+  wave_lds_sync();
+}
+
+template <class G>
+__device__ __forceinline__ float tplane(const int8_t* stone, const uint8_t* invd, const BoardMeta& m, int c, int j) {
+  switch (c) {
+    case 0: return stone[j] == 1 ? 1.f : 0.f;
+    case 1: return stone[j] == 2 ? 1.f : 0.f;
+    case 2: return (float)m.turn;
+    case 3: return (float)invd[j];
+    case 4: return (float)m.passed;
+    default: return (float)m.done;
+  }
+}
+
+// representation input board + root mask from 6 observation planes plane(c, cell)
+template <class G, class PlaneFn>
+__device__ __forceinline__ void tstage_root(const TowerArrays& T, int g, double pass_epsilon, PlaneFn plane) {
+  bf16* dst = T.rep_in + (size_t)g * G::P * 64;
+  for (int i = threadIdx.x; i < G::CELLS * 8; i += 64) {
+    const int p = i >> 3, j = i & 7;
+    const int y = p / G::N, x = p - y * G::N;
+    const int q = (y + 1) * G::W + (x + 1);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)((j == 0 && k < 6) ? plane(k, p) : 0.f);
+    *reinterpret_cast<bf16x8*>(dst + tpix(q, j)) = o;
+  }
+  int any = 0;
+  for (int a = threadIdx.x; a < G::A; a += 64) {
+    const uint8_t v = a < G::CELLS ? (plane(3, a) == 0.f ? 1 : 0) : 1;
+    T.rootmask[(size_t)g * G::A + a] = v;
+    any |= (a < G::CELLS) && v;
+  }
+  any = __any(any);
+  if (threadIdx.x == 0) T.passp[g] = any ? pass_epsilon : 1.0;
+}
+
+// self-play move start: observation record, representation input, root mask
+template <int N>
+__global__ void __launch_bounds__(64) k_tobs(TowerArrays T, SearchParams sp, PlayParams pp, EngineArrays E) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  __shared__ int8_t stone[G::CELLS];
+  __shared__ uint8_t invd[G::CELLS];
+  if (E.status[g] != 0) { if (threadIdx.x == 0) T.playing[g] = 0; return; }
+  for (int c = threadIdx.x; c < G::CELLS; c += 64) {
+    stone[c] = E.stones[(size_t)g * G::CELLS + c];
+    invd[c] = E.invd[(size_t)g * G::CELLS + c];
+  }
+  BoardMeta m;
+  const int* mm = E.meta + g * 4;
+  m.turn = mm[0]; m.passed = mm[1]; m.done = mm[2]; m.moves = mm[3];
+  wave_lds_sync();
+  const size_t rec = (size_t)g * E.max_moves + m.moves;
+  for (int c = threadIdx.x; c < G::CELLS; c += 64) {
+    E.rec_stones[rec * G::CELLS + c] = stone[c];
+    E.rec_invd[rec * G::CELLS + c] = invd[c];
+  }
+  if (threadIdx.x == 0) {
+    E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
+    T.playing[g] = 1;
+    const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
+    T.key[g] = stream_key(sp.seed, gid, (uint32_t)m.moves);
+  }
+  tstage_root<G>(T, g, sp.pass_epsilon, [&](int c, int j) { return tplane<G>(stone, invd, m, c, j); });
+}
+
+// search API start: root observations f32 [G][6][N][N]
+template <int N>
+__global__ void __launch_bounds__(64) k_tobs_search(TowerArrays T, SearchParams sp, const float* __restrict__ obs,
+                                                    int game_base, int move_index) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  const float* o = obs + (size_t)g * 6 * G::CELLS;
+  if (threadIdx.x == 0) {
+    T.playing[g] = 1;
+    T.key[g] = stream_key(sp.seed, (uint32_t)(game_base + g), (uint32_t)move_index);
+  }
+  tstage_root<G>(T, g, sp.pass_epsilon, [&](int c, int j) { return o[c * G::CELLS + j]; });
+}
+
+// root priors (self_play.py:148-182) from the representation's heads, tree reset
+template <int N>
+__global__ void __launch_bounds__(64) k_troot(TowerArrays T, SearchParams sp, EngineArrays E,
+                                              const double* __restrict__ noise, long long game_stride,
+                                              int per_move) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  if (!T.playing[g]) return;
+  __shared__ TreeLds<G> t;
+  __shared__ float hp[3 * G::CS];
+  tload_mask<G>(t, T, g);
+  stage_head_scalars(T.hs, t.hsc);
+  tsum_heads<G>(T, g, hp);
+  // representation: no reward head; value, then policy (rows 1, 2 of hp)
+  heads_logits<G, 1>(hp + G::CS, false, t.hsc, t.logits);
+  wave_lds_sync();
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  // injected Dirichlet samples (test hook): [G][A] (search) or [G][M][A] (self-play)
+  const double* nz = noise ? noise + (size_t)g * game_stride + (per_move ? (size_t)E.meta[g * 4 + 3] * G::A : 0)
+                           : nullptr;
+  root_priors<G>(t, TV, sp, nz, T.key[g]);
+  TreeAcc<G, false> acc(TV, t);
+  tree_reset_root<G>(acc);
+  if (threadIdx.x == 0) { E.nodes[g] = 1; T.simc[g] = 0; }
+}
+
+// select_leaf for one simulation of every game -> the conv jobs
+template <int N>
+__global__ void __launch_bounds__(64) k_tselect(TowerArrays T, SearchParams sp, EngineArrays E) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  if (!T.playing[g]) { if (threadIdx.x == 0) T.evalact[g] = 0; return; }
+  __shared__ TreeLds<G> t;
+  tload_mask<G>(t, T, g);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  TreeAcc<G, false> acc(TV, t);
+  const int sim = T.simc[g];
+  const int a = select_leaf<G>(t, acc, sp, T.key[g], sim);
+  if (a >= 0) {
+    const int nid = E.nodes[g];
+    if (threadIdx.x == 0) {
+      const int base = g * (E.S + 1);
+      T.in_idx[g] = base + t.leaf;
+      T.out_idx[g] = base + nid;
+      T.act[g] = a;
+      T.job[g * 3] = t.leaf; T.job[g * 3 + 1] = t.depth; T.job[g * 3 + 2] = nid;
+      T.evalact[g] = 1;
+    }
+  } else {
+    // self_play.py: a terminal leaf backs up 0 (:188-191); main.py: nothing (:296)
+    if (a == -1) backup<G>(acc, t.depth, -1, 0.0);
+    if (threadIdx.x == 0) { T.evalact[g] = 0; T.simc[g] = sim + 1; }
+  }
+}
+
+// heads -> the new node's child priors, reward / value -> backup (:198-230)
+template <int N>
+__global__ void __launch_bounds__(64) k_texpand(TowerArrays T, SearchParams sp, EngineArrays E) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  if (!T.evalact[g]) return;
+  __shared__ TreeLds<G> t;
+  __shared__ float hp[3 * G::CS];
+  tload_mask<G>(t, T, g);
+  stage_head_scalars(T.hs, t.hsc);
+  tsum_heads<G>(T, g, hp);
+  const int leaf = T.job[g * 3], depth = T.job[g * 3 + 1], nid = T.job[g * 3 + 2], a = T.act[g];
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  TreeAcc<G, false> acc(TV, t);
+  float r, v;
+  heads_value<G, 1>(hp, true, t.hsc, r, v);
+  float x[G::AP];
+  logits_regs<G, 1>(hp, true, t.hsc, x);
+  int* crow = TV.child + (size_t)nid * G::A;
+  for (int i = threadIdx.x; i < G::A; i += 64) crow[i] = -1;
+  child_priors<G>(t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant);
+  if (threadIdx.x == 0) acc.init(nid);
+  if (threadIdx.x == (a & 63)) acc.set_child(leaf, a, nid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  backup<G>(acc, depth, nid, (double)r + sp.discount * (double)v, sp.variant == 0);
+  if (threadIdx.x == 0) { E.nodes[g] = nid + 1; T.simc[g] += 1; }
+}
+
+// action choice, record, board step (self_play.py:465-507), as k_selfplay_move's tail
+template <int N>
+__global__ void __launch_bounds__(64) k_tchoose(TowerArrays T, SearchParams sp, PlayParams pp, EngineArrays E) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  if (!T.playing[g]) return;
+  __shared__ TreeLds<G> t;
+  __shared__ int8_t stone[G::CELLS];
+  __shared__ uint8_t invd[G::CELLS];
+  __shared__ int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS];
+  __shared__ int killed[4], misc[8];
+  tload_mask<G>(t, T, g);
+  for (int c = threadIdx.x; c < G::CELLS; c += 64) {
+    stone[c] = E.stones[(size_t)g * G::CELLS + c];
+    invd[c] = E.invd[(size_t)g * G::CELLS + c];
+  }
+  BoardMeta m;
+  const int* mm = E.meta + g * 4;
+  m.turn = mm[0]; m.passed = mm[1]; m.done = mm[2]; m.moves = mm[3];
+  const int mv = m.moves;
+  const size_t rec = (size_t)g * E.max_moves + mv;
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  const uint64_t key = T.key[g];
+  const double temp = mv < pp.temperature_moves ? pp.temperature : 0.0;
+  const int a = sp.variant == 1 ? choose_action_main<G>(t, TV, key, E.rec_policy + rec * G::A)
+                                : choose_action<G>(t, TV, sp.compat, temp, key, E.rec_policy + rec * G::A);
+  if (threadIdx.x == 0) {
+    E.rec_action[rec] = a;
+    const int n = TV.visits[0];
+    E.rec_value[rec] = n > 0 ? TV.wsum[0] / (double)n : 0.0;
+  }
+  __syncthreads();
+  BoardLds<G> bl;
+  bl.stone = stone; bl.invd = invd; bl.label = label; bl.libs = libs; bl.gsize = gsize;
+  bl.killed = killed; bl.misc = misc;
+  const int st = board_step<G>(bl, m, a);
+  __syncthreads();
+  double w = 0.0;
+  if (st == BOARD_OK && m.done) w = board_winning<G>(bl, pp.komi);
+  for (int c = threadIdx.x; c < G::CELLS; c += 64) {
+    E.stones[(size_t)g * G::CELLS + c] = stone[c];
+    E.invd[(size_t)g * G::CELLS + c] = invd[c];
+  }
+  if (threadIdx.x == 0) {
+    int* mw = E.meta + g * 4;
+    mw[0] = m.turn; mw[1] = m.passed; mw[2] = m.done; mw[3] = m.moves;
+    E.rec_reward[rec] = w;
+    atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);
+    atomicAdd(&E.counters[1], 1ull);
+    atomicAdd(&E.counters[3], (unsigned long long)sp.num_simulations);   // a tower per simulation
+    if (st != BOARD_OK) {
+      E.status[g] = 16 + st;
+    } else if (m.done || m.moves >= E.max_moves) {
+      E.status[g] = 1;
+      E.game_len[g] = m.moves;
+      E.final_reward[g] = m.done ? w : 0.0;
+      atomicAdd(&E.counters[2], 1ull);
+    }
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(64) k_tsearch_out(EngineArrays E, int* out_visits, double* out_value) {
+  search_outputs<TGeo<N>>(E, blockIdx.x, out_visits, out_value);
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in inference plumbing: f32 NCHW <-> bf16 chunked boards, heads.
+// ---------------------------------------------------------------------------
+// latent f32 [B][C][N][N] -> boards (C channels); obs f32 [B][6][N][N] ->
+// one 64-channel chunk (6 planes + zeros) when obs6
+template <int N>
+__global__ void __launch_bounds__(256) k_tin(const float* __restrict__ src, bf16* dst, int C, int obs6,
+                                             long long dst_stride) {
+  typedef TGeo<N> G;
+  const int b = blockIdx.x;
+  const int CC = obs6 ? 1 : C / 64, CIN = obs6 ? 6 : C;
+  const float* s = src + (size_t)b * CIN * G::CELLS;
+  bf16* d = dst + (size_t)b * dst_stride;
+  for (int i = threadIdx.x; i < CC * G::CELLS * 8; i += 256) {
+    const int cc = i / (G::CELLS * 8), r = i - cc * G::CELLS * 8;
+    const int p = r >> 3, j = r & 7;
+    const int y = p / N, x = p - y * N;
+    const int q = (y + 1) * G::W + (x + 1);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = cc * 64 + j * 8 + k;
+      o[k] = (bf16)(c < CIN ? s[(size_t)c * G::CELLS + p] : 0.f);
+    }
+    *reinterpret_cast<bf16x8*>(d + (size_t)cc * G::P * 64 + tpix(q, j)) = o;
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) k_tout(const bf16* __restrict__ src, float* dst, int C) {
+  typedef TGeo<N> G;
+  const int b = blockIdx.x;
+  const int CC = C / 64;
+  const bf16* s = src + (size_t)b * CC * G::P * 64;
+  float* d = dst + (size_t)b * C * G::CELLS;
+  for (int i = threadIdx.x; i < CC * G::CELLS * 8; i += 256) {
+    const int cc = i / (G::CELLS * 8), r = i - cc * G::CELLS * 8;
+    const int p = r >> 3, j = r & 7;
+    const int y = p / N, x = p - y * N;
+    const int q = (y + 1) * G::W + (x + 1);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(s + (size_t)cc * G::P * 64 + tpix(q, j));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[(size_t)(cc * 64 + j * 8 + k) * G::CELLS + p] = (float)v[k];
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(64) k_theads(TowerArrays T, int has_reward, float* reward, float* value,
+                                               float* logits) {
+  typedef TGeo<N> G;
+  const int b = blockIdx.x;
+  __shared__ float hp[3 * G::CS];
+  __shared__ float hsc[64];
+  stage_head_scalars(T.hs, hsc);
+  tsum_heads<G>(T, b, hp);
+  const float* h = has_reward ? hp : hp + G::CS;
+  float r, v;
+  heads_value<G, 1>(h, has_reward != 0, hsc, r, v);
+  heads_logits<G, 1>(h, has_reward != 0, hsc, logits + (size_t)b * G::A);
+  if (threadIdx.x == 0) {
+    value[b] = v;
+    if (has_reward) reward[b] = r;
+  }
+}
+
+}  // namespace mzgo

@@ -1,0 +1,244 @@
+// mzgo_tower_host.hpp -- host side of the residual-tower engine (BASELINE
+// config 5): the state_dict of mzgo/resnet.py's ResMuZeroNet, weight packing,
+// device buffers and the launch sequences of a move / a search / the
+// drop-in inference calls.  Included by mzgo_capi.hip (the engine owns one
+// TowerHost when mzgo_config.tower is 1).
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "mzgo_tower_dispatch.hpp"
+
+namespace mzgo {
+
+// f32 -> bf16 bits, round to nearest even (the device's v_cvt_pk_bf16_f32)
+inline uint16_t bf16_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+inline float bf16_round(float f) {
+  uint32_t u = (uint32_t)bf16_bits(f) << 16;
+  float r;
+  std::memcpy(&r, &u, 4);
+  return r;
+}
+
+// conv weight W[cout][cin][3][3] (f32) -> bf16 tiles [co chunk][ci chunk][tap][64 cout][64 cin],
+// the 16-byte pieces of row r at position piece ^ ((r >> 1) & 7) (mzgo_tower.hpp)
+inline std::vector<uint16_t> pack_tconv(const float* W, int COUT, int CIN) {
+  const int CO = COUT / 64, CI = (CIN + 63) / 64;
+  std::vector<uint16_t> out((size_t)CO * CI * 9 * 64 * 64, 0);
+  for (int cg = 0; cg < CO; ++cg)
+    for (int cc = 0; cc < CI; ++cc)
+      for (int t = 0; t < 9; ++t)
+        for (int r = 0; r < 64; ++r)
+          for (int k = 0; k < 64; ++k) {
+            const int co = cg * 64 + r, ci = cc * 64 + k;
+            const float v = ci < CIN ? W[((size_t)co * CIN + ci) * 9 + t] : 0.f;
+            const size_t tile = (((size_t)cg * CI + cc) * 9 + t) * 64 * 64;
+            out[tile + (size_t)r * 64 + (((k >> 3) ^ ((r >> 1) & 7)) << 3) + (k & 7)] = bf16_bits(v);
+          }
+  return out;
+}
+
+struct TowerHost {
+  int N = 0, C = 0, CC = 0, blocks = 0, G = 0, S = 0, A = 0, P = 0, CS = 0;
+  const TowerSet* ts = nullptr;
+  // device buffers (owned by the engine's allocation list)
+  TowerArrays TA{};
+  bf16* t0 = nullptr; bf16* t1 = nullptr;
+  // drop-in inference scratch, grown on demand
+  bf16* ib = nullptr; bf16* ob = nullptr; bf16* s0 = nullptr; bf16* s1 = nullptr;
+  float* shp = nullptr; int* sact = nullptr;
+  int scap = 0;
+  // weights
+  void* d_wb = nullptr; size_t d_wb_bytes = 0;        // bf16 conv tiles
+  float* d_wf = nullptr; size_t d_wf_bytes = 0;       // f32: biases, E table, heads, scalars
+  struct Conv { const bf16* w; const float* b; int cin_chunks; };
+  std::vector<Conv> rep, dyn;                         // conv_in then (conv1, conv2) per block
+  const float* etab = nullptr;
+  HeadScalars hs{};
+
+  long long slot() const { return (long long)CC * P * 64; }
+
+  static std::vector<std::pair<std::string, std::vector<int64_t>>> specs(int C, int A, int blocks) {
+    std::vector<std::pair<std::string, std::vector<int64_t>>> s;
+    auto conv = [&](const std::string& k, int64_t co, int64_t ci) {
+      s.push_back({k + ".weight", {co, ci, 3, 3}});
+      s.push_back({k + ".bias", {co}});
+    };
+    conv("representation.conv_in", C, 6);
+    for (int i = 0; i < blocks; ++i) {
+      conv("representation.blocks." + std::to_string(i) + ".conv1", C, C);
+      conv("representation.blocks." + std::to_string(i) + ".conv2", C, C);
+    }
+    s.push_back({"dynamics.action_embedding.weight", {A, C}});
+    conv("dynamics.conv_in", C, C);
+    for (int i = 0; i < blocks; ++i) {
+      conv("dynamics.blocks." + std::to_string(i) + ".conv1", C, C);
+      conv("dynamics.blocks." + std::to_string(i) + ".conv2", C, C);
+    }
+    s.push_back({"dynamics.reward_conv.weight", {1, C, 1, 1}});
+    s.push_back({"dynamics.reward_conv.bias", {1}});
+    s.push_back({"dynamics.fc_reward_hidden.weight", {16, 1}});
+    s.push_back({"dynamics.fc_reward_hidden.bias", {16}});
+    s.push_back({"dynamics.fc_reward_output.weight", {1, 16}});
+    s.push_back({"dynamics.fc_reward_output.bias", {1}});
+    s.push_back({"prediction.pass_logit", {1}});
+    s.push_back({"prediction.value_conv.weight", {1, C, 1, 1}});
+    s.push_back({"prediction.value_conv.bias", {1}});
+    s.push_back({"prediction.value_fc.weight", {1, 1}});
+    s.push_back({"prediction.value_fc.bias", {1}});
+    s.push_back({"prediction.policy_conv.weight", {1, C, 1, 1}});
+    s.push_back({"prediction.policy_conv.bias", {1}});
+    return s;
+  }
+
+  // pack + upload (host f32 state_dict -> device).  The dynamics' first conv
+  // adds the action embedding through the region table of mzgo_expand.hpp
+  // (conv(x + emb[a]) = conv(x) + E[a][region] under zero padding), built from
+  // the bf16-rounded weights the MFMA uses: the GEMM never sees emb.
+  hipError_t upload(std::map<std::string, std::vector<float>>& sd,
+                    std::vector<float> (*taps)(const float*, const float*, int, int)) {
+    std::vector<uint16_t> wb;
+    std::vector<size_t> woff;
+    std::vector<std::string> order;
+    auto addw = [&](const std::string& k, int cin) {
+      woff.push_back(wb.size());
+      order.push_back(k);
+      std::vector<uint16_t> p = pack_tconv(sd[k + ".weight"].data(), C, cin);
+      wb.insert(wb.end(), p.begin(), p.end());
+    };
+    addw("representation.conv_in", 6);
+    for (int i = 0; i < blocks; ++i) {
+      addw("representation.blocks." + std::to_string(i) + ".conv1", C);
+      addw("representation.blocks." + std::to_string(i) + ".conv2", C);
+    }
+    addw("dynamics.conv_in", C);
+    for (int i = 0; i < blocks; ++i) {
+      addw("dynamics.blocks." + std::to_string(i) + ".conv1", C);
+      addw("dynamics.blocks." + std::to_string(i) + ".conv2", C);
+    }
+    std::vector<float> wf;
+    auto addf = [&](const std::vector<float>& v) {
+      const size_t o = wf.size();
+      wf.insert(wf.end(), v.begin(), v.end());
+      wf.resize((wf.size() + 63) / 64 * 64, 0.f);
+      return o;
+    };
+    std::vector<size_t> boff;
+    for (const std::string& k : order) boff.push_back(addf(sd[k + ".bias"]));
+    std::vector<float> wr = sd["dynamics.conv_in.weight"];
+    for (float& x : wr) x = bf16_round(x);
+    const size_t eoff = addf(taps(wr.data(), sd["dynamics.action_embedding.weight"].data(), C, A));
+    std::vector<float> hw;
+    for (const char* k : {"dynamics.reward_conv.weight", "prediction.value_conv.weight",
+                          "prediction.policy_conv.weight"})
+      hw.insert(hw.end(), sd[k].begin(), sd[k].end());
+    const size_t hoff = addf(hw);
+    const char* scal[] = {"dynamics.reward_conv.bias", "dynamics.fc_reward_hidden.weight",
+                          "dynamics.fc_reward_hidden.bias", "dynamics.fc_reward_output.weight",
+                          "dynamics.fc_reward_output.bias", "prediction.value_conv.bias",
+                          "prediction.value_fc.weight", "prediction.value_fc.bias",
+                          "prediction.policy_conv.bias", "prediction.pass_logit"};
+    std::vector<size_t> soff;
+    for (const char* k : scal) soff.push_back(addf(sd[k]));
+    hipError_t e;
+    if (wb.size() * 2 > d_wb_bytes) {
+      if (d_wb) (void)hipFree(d_wb);
+      d_wb = nullptr;
+      if ((e = hipMalloc(&d_wb, wb.size() * 2)) != hipSuccess) return e;
+      d_wb_bytes = wb.size() * 2;
+    }
+    if (wf.size() * 4 > d_wf_bytes) {
+      if (d_wf) (void)hipFree(d_wf);
+      d_wf = nullptr;
+      if ((e = hipMalloc(&d_wf, wf.size() * 4)) != hipSuccess) return e;
+      d_wf_bytes = wf.size() * 4;
+    }
+    if ((e = hipMemcpy(d_wb, wb.data(), wb.size() * 2, hipMemcpyHostToDevice)) != hipSuccess) return e;
+    if ((e = hipMemcpy(d_wf, wf.data(), wf.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return e;
+    const bf16* bw = reinterpret_cast<const bf16*>(d_wb);
+    rep.clear();
+    dyn.clear();
+    const int nrep = 1 + 2 * blocks;
+    for (size_t i = 0; i < order.size(); ++i) {
+      Conv c{bw + woff[i], d_wf + boff[i], (i == 0) ? 1 : CC};
+      if ((int)i < nrep) rep.push_back(c); else dyn.push_back(c);
+    }
+    etab = d_wf + eoff;
+    TA.headw = d_wf + hoff;
+    const float* f = d_wf;
+    hs.reward_b = f + soff[0]; hs.fc1_w = f + soff[1]; hs.fc1_b = f + soff[2]; hs.fc2_w = f + soff[3];
+    hs.fc2_b = f + soff[4]; hs.value_b = f + soff[5]; hs.vfc_w = f + soff[6]; hs.vfc_b = f + soff[7];
+    hs.policy_b = f + soff[8]; hs.pass_logit = f + soff[9];
+    TA.hs = hs;
+    return hipSuccess;
+  }
+
+  // One tower over nb boards: conv_in (in -> t0, or straight to out without
+  // blocks), then per block conv1 (t0 -> t1) and conv2 (t1 + t0 -> t0; the
+  // last block's into out) with the fused heads on the final conv.
+  hipError_t tower(const std::vector<Conv>& L, const bf16* in, const int* in_idx, long long in_stride, bf16* out,
+                   const int* out_idx, long long out_stride, const int* act, const int* active, int nb, bf16* a0,
+                   bf16* a1, float* hpart, hipStream_t s) const {
+    TConvArgs c{};
+    c.nboards = nb;
+    c.co_chunks = CC;
+    c.active = active;
+    const long long sl = slot();
+    hipError_t e;
+    auto run = [&](const Conv& cv, const bf16* src, const int* sidx, long long sstr, bf16* dst, const int* didx,
+                   long long dstr, const bf16* res, bool heads, const float* et) {
+      c.in = src; c.in_idx = sidx; c.in_stride = sstr;
+      c.out = dst; c.out_idx = didx; c.out_stride = dstr;
+      c.res = res; c.res_idx = nullptr; c.res_stride = sl;
+      c.w = cv.w; c.bias = cv.b; c.ci_chunks = cv.cin_chunks;
+      c.etab = et; c.act = et ? act : nullptr;
+      c.headw = heads ? TA.headw : nullptr; c.hpart = hpart;
+      return ts->conv(c, s);
+    };
+    const int nb_ = (int)(L.size() - 1) / 2;
+    const float* et = act ? etab : nullptr;
+    if (nb_ == 0) return run(L[0], in, in_idx, in_stride, out, out_idx, out_stride, nullptr, true, et);
+    if ((e = run(L[0], in, in_idx, in_stride, a0, nullptr, sl, nullptr, false, et)) != hipSuccess) return e;
+    for (int k = 0; k < nb_; ++k) {
+      const bool lastb = k == nb_ - 1;
+      if ((e = run(L[1 + 2 * k], a0, nullptr, sl, a1, nullptr, sl, nullptr, false, nullptr)) != hipSuccess) return e;
+      if ((e = run(L[2 + 2 * k], a1, nullptr, sl, lastb ? out : a0, lastb ? out_idx : nullptr,
+                   lastb ? out_stride : sl, a0, lastb, nullptr)) != hipSuccess)
+        return e;
+    }
+    return hipSuccess;
+  }
+
+  // representation tower + root priors for the slots marked playing
+  hipError_t root_phase(const SearchParams& sp, const EngineArrays& E, const double* noise, long long nstride,
+                        int per_move, hipStream_t s) const {
+    hipError_t e;
+    if ((e = tower(rep, TA.rep_in, nullptr, (long long)P * 64, TA.pool, TA.root_idx, slot(), nullptr, TA.playing, G,
+                   t0, t1, TA.hpart, s)) != hipSuccess)
+      return e;
+    return ts->root(TA, sp, E, noise, nstride, per_move, G, s);
+  }
+
+  // S simulations: select (all games) -> dynamics tower (all leaves) -> expand + backup
+  hipError_t simulations(const SearchParams& sp, const EngineArrays& E, hipStream_t s) const {
+    hipError_t e;
+    for (int i = 0; i < S; ++i) {
+      if ((e = ts->select(TA, sp, E, G, s)) != hipSuccess) return e;
+      if ((e = tower(dyn, TA.pool, TA.in_idx, slot(), TA.pool, TA.out_idx, slot(), TA.act, TA.evalact, G, t0, t1,
+                     TA.hpart, s)) != hipSuccess)
+        return e;
+      if ((e = ts->expand(TA, sp, E, G, s)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+};
+
+}  // namespace mzgo

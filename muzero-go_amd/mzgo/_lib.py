@@ -40,6 +40,8 @@ class Config(ctypes.Structure):
         ("game_base", ctypes.c_int),
         ("device", ctypes.c_int),
         ("direct_dynamics", ctypes.c_int),
+        ("tower", ctypes.c_int),
+        ("res_blocks", ctypes.c_int),
     ]
 
 

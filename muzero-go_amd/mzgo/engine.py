@@ -37,6 +37,8 @@ class EngineConfig:
     game_base: int = 0
     device: int = 0
     dynamics: str = "factored"    # "factored" (conv once per parent, mzgo_expand.hpp) or "direct"
+    tower: int = 0                # 1: the residual-tower network (BASELINE config 5, mzgo.resnet)
+    res_blocks: int = 0           # its residual blocks per network
 
     def to_c(self):
         c = _lib.Config()

@@ -15,6 +15,7 @@ import torch
 
 from .engine import EngineConfig
 from .net import MuZeroNet
+from .resnet import ResMuZeroNet
 
 
 class TreeNode:
@@ -63,8 +64,8 @@ class MCTS:
     def __init__(self, muzero_net, action_size, num_simulations, c_puct=2.5, *, compat="reference",
                  seed=1234, game=0, dirichlet_alpha=0.15, dirichlet_epsilon=0.02, discount=0.99,
                  pass_epsilon=0.01, dynamics="factored"):
-        if not isinstance(muzero_net, MuZeroNet):
-            raise TypeError("mzgo.MCTS searches with an mzgo.MuZeroNet (HIP engine); got "
+        if not isinstance(muzero_net, (MuZeroNet, ResMuZeroNet)):
+            raise TypeError("mzgo.MCTS searches with an mzgo.MuZeroNet or ResMuZeroNet (HIP engine); got "
                             f"{type(muzero_net).__name__}")
         if action_size != muzero_net.board_size ** 2 + 1:
             raise ValueError("action_size must be the board's N*N+1 actions")

@@ -1,0 +1,141 @@
+"""GPU parity of the residual-tower engine (BASELINE config 5; no reference
+counterpart, so the parity reference is the build's own architecture,
+oracle/resnet.py).
+
+Tolerances (bf16 MFMA operands, fp32 accumulation, bf16 activations):
+* vs ``OracleResNet(bf16=True)`` -- the engine's rounding points in float64,
+  so only the fp32 summation order differs (an element now and then rounds to
+  the neighbouring bf16 value and the difference propagates through the
+  tower): latents |diff| <= 0.03 (max) and mean |diff| <= 1e-3 of the mean
+  |latent|; value / reward / logits |diff| <= 0.02.
+* vs ``OracleResNet(bf16=False)`` -- the architecture in fp32: the bf16
+  error itself, |diff| <= 0.05 + 0.05 |ref| on every output.
+* search trees vs oracle.mcts.MCTS driven by the bf16-rounding oracle with
+  the same counter streams and injected Dirichlet noise: identical root-child
+  visit counts, root value within 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gogame as gg
+
+pytestmark = pytest.mark.gpu
+
+
+def _nets(N, C, blocks, seed=0):
+    import mzgo
+    from oracle.resnet import OracleResNet
+    A = N * N + 1
+    sd = mzgo.deterministic_res_state_dict(C, A, blocks, seed)
+    net = mzgo.ResMuZeroNet(C, A, blocks).to("cuda").eval()
+    net.load_state_dict(sd)
+    return net, OracleResNet(sd, blocks, bf16=True), OracleResNet(sd, blocks, bf16=False)
+
+
+def _boards(N, B, seed=0):
+    from oracle.positions import random_position
+    rng = np.random.default_rng(seed)
+    return np.stack([random_position(N, int(rng.integers(0, N * N // 2)), int(rng.integers(1 << 30)))
+                     for _ in range(B)]).astype(np.float32)
+
+
+def _close_latent(got, want):
+    d = (got - want).abs()
+    assert d.max().item() <= 0.03, d.max().item()
+    assert d.mean().item() <= 1e-3 * max(want.abs().mean().item(), 1e-3), (d.mean().item(), want.abs().mean().item())
+
+
+@pytest.mark.parametrize("N,C,blocks", [(5, 64, 0), (5, 64, 2), (9, 128, 1), (19, 64, 1), (19, 256, 2)])
+def test_tower_inference_matches_oracle(N, C, blocks):
+    net, emu, f32 = _nets(N, C, blocks)
+    A = N * N + 1
+    B = 6
+    obs = torch.from_numpy(_boards(N, B))
+    lat, v, lg = net.initial_inference(obs.cuda())
+    with torch.no_grad():
+        elat, ev, elg = emu.initial_inference(obs)
+        flat, fv, flg = f32.initial_inference(obs)
+    _close_latent(lat.cpu(), elat)
+    np.testing.assert_allclose(v.cpu().numpy(), ev.numpy(), atol=0.02)
+    np.testing.assert_allclose(lg.cpu().numpy(), elg.numpy(), atol=0.02)
+    for got, want in ((lat, flat), (v, fv), (lg, flg)):
+        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), atol=0.05, rtol=0.05)
+    act = torch.tensor([0, A - 1, 3, A // 2, 1, 2])[:B]
+    nl, r, v2, lg2 = net.recurrent_inference(lat, act.cuda())
+    with torch.no_grad():
+        enl, er, ev2, elg2 = emu.recurrent_inference(lat.cpu(), act)
+        fnl, fr, fv2, flg2 = f32.recurrent_inference(lat.cpu(), act)
+    _close_latent(nl.cpu(), enl)
+    for got, want in ((r, er), (v2, ev2), (lg2, elg2)):
+        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), atol=0.02)
+    for got, want in ((nl, fnl), (r, fr), (v2, fv2), (lg2, flg2)):
+        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), atol=0.05, rtol=0.05)
+
+
+@pytest.mark.parametrize("N,C,blocks,S", [(5, 64, 1, 25), (9, 64, 1, 120)])
+def test_tower_search_matches_oracle_tree(N, C, blocks, S):
+    import mzgo
+    from oracle.mcts import MCTS as OracleMCTS, tree_summary
+    from oracle.rng import SearchHooks, injected_noise
+    net, emu, _ = _nets(N, C, blocks)
+    A = N * N + 1
+    seed, game, move = 7, 3, 11
+    obs = _boards(N, 1, seed=5)[0].astype(np.float64)
+    noise = injected_noise(seed, game, move, A)
+    m = mzgo.MCTS(net, A, S, seed=seed, game=game)
+    root, _, value = m.run(obs, move_index=move, noise=torch.from_numpy(noise))
+    hooks = SearchHooks(seed, game, move)
+    om = OracleMCTS(emu, A, S, choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+                    noise=lambda p, a, e: (1 - e) * p + e * noise)
+    with torch.no_grad():
+        oroot, _, ovalue = om.run(obs)
+    visits, _ = tree_summary(oroot, A)
+    np.testing.assert_array_equal(m.root_child_visits, visits)
+    assert abs(value - ovalue) < 1e-3, (value, ovalue)
+
+
+def test_tower_selfplay_games_on_oracle_board():
+    """Whole 5x5 games on the tower engine: every recorded observation equals
+    the oracle board replaying the recorded actions, every action legal, the
+    compat policy target, counters consistent."""
+    import mzgo
+    from oracle.mcts import root_valid_mask
+    N, C, blocks, G, S = 5, 64, 1, 8, 12
+    net, _, _ = _nets(N, C, blocks)
+    sp = mzgo.SelfPlay(net, G, S, seed=3)
+    c0 = sp.engine.counters()
+    hists = sp.play()
+    c = sp.engine.counters()
+    assert c["playing"] == 0
+    moves = sum(len(h) for h in hists)
+    assert c["moves"] - c0["moves"] == moves and c["simulations"] - c0["simulations"] == moves * S
+    for h in hists:
+        st = gg.init_state(N)
+        for obs, a, pol in zip(h.observations, h.actions, h.policies):
+            np.testing.assert_array_equal(obs, st)
+            mask = root_valid_mask(obs)
+            assert mask[a] > 0
+            np.testing.assert_array_equal(pol, mask / mask.sum())
+            st = gg.next_state(st, a)
+        assert len(h) == N * N or gg.game_ended(st)
+
+
+def test_tower_config5_shapes_one_move():
+    """BASELINE config 5's shapes (19x19, C=256, 20 blocks) for 8 games x 4
+    simulations: one move completes with finite values and legal actions."""
+    import mzgo
+    N, C, blocks, G, S = 19, 256, 20, 8, 4
+    A = N * N + 1
+    net = mzgo.ResMuZeroNet(C, A, blocks).to("cuda").eval()
+    net.load_state_dict(mzgo.deterministic_res_state_dict(C, A, blocks, 0))
+    sp = mzgo.SelfPlay(net, G, S, seed=1)
+    sp.reset()
+    sp.move()
+    torch.cuda.synchronize()
+    for g in range(G):
+        r = sp.engine.record(g)
+        assert r["length"] == 1
+        assert np.isfinite(r["value"]).all()
+        st = gg.init_state(N)
+        assert gg.invalid_moves(st)[int(r["action"][0])] == 0 or int(r["action"][0]) == N * N
