@@ -36,9 +36,10 @@ def mfma_per_conv(N, cin, cout):
     return 9 * (cin // 4) * (cout // 16) * ((N * N + 15) // 16)
 
 
-def cpu_baseline(N, C, S, budget_s=12.0):
+def cpu_baseline(N, C, S, budget_s=12.0, blocks=None):
     """The oracle (CPU restatement of self_play.py's MCTS, batch-1 torch net,
-    object tree) timed on this host with one thread, on a bounded sample."""
+    object tree) timed on this host with one thread, on a bounded sample.
+    blocks: the residual-tower network of config 5 (oracle/resnet.py, fp32)."""
     import numpy as np
 
     from oracle.mcts import MCTS
@@ -49,41 +50,51 @@ def cpu_baseline(N, C, S, budget_s=12.0):
 
     torch.set_num_threads(1)
     A = N * N + 1
-    net = OracleNet(deterministic_state_dict(C, A, 0))
+    if blocks is None:
+        net = OracleNet(deterministic_state_dict(C, A, 0))
+    else:
+        from mzgo.weights import deterministic_res_state_dict
+        from oracle.resnet import OracleResNet
+        net = OracleResNet(deterministic_res_state_dict(C, A, blocks, 0), blocks)
     st = gogame.init_state(N)
     sims, moves, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         hooks = SearchHooks(1234, 0, moves)
         noise = injected_noise(1234, 0, moves, A)
+        # a search cut short at the budget counts the simulations it ran
+        left = budget_s - (time.perf_counter() - t0)
         m = MCTS(net, A, S, choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
                  noise=lambda p, a, e: (1 - e) * p + e * noise)
+        if blocks is not None:
+            m.num_simulations = S if left > 60 else max(1, min(S, int(left / 0.3)))
         with torch.no_grad():
             m.run(st)
-        sims += S
+        sims += m.num_simulations
         legal = np.flatnonzero(gogame.invalid_moves(st) == 0)
         st = gogame.next_state(st, int(legal[moves % len(legal)]))
         moves += 1
         if gogame.game_ended(st):
             st = gogame.init_state(N)
     dt = time.perf_counter() - t0
+    net_name = "batch-1 net" if blocks is None else f"{blocks}-block residual net (fp32), batch 1"
     return {"value": sims / dt, "unit": "sims/s", "cores": 1, "kind": "port",
-            "sample": f"{moves} moves x {S} sims, {N}x{N}, one game, 1 thread, {dt:.1f} s "
-                      f"(oracle MCTS + torch-CPU batch-1 net; host has {os.cpu_count()} cpus)"}
+            "sample": f"{moves} moves, {sims} sims, {N}x{N}, one game, 1 thread, {dt:.1f} s "
+                      f"(oracle MCTS + torch-CPU {net_name}; host has {os.cpu_count()} cpus)"}
 
 
 def _cpu_worker(a):
     return cpu_baseline(*a)
 
 
-def cpu_baseline_procs(N, C, S, budget_s, procs):
+def cpu_baseline_procs(N, C, S, budget_s, procs, blocks=None):
     """P independent single-thread oracle processes (the
     reference's own parallelism is one game per process), sims/s summed.
     Must run before this process touches the GPU (spawned children)."""
     import multiprocessing as mp
     if procs <= 1:
-        return cpu_baseline(N, C, S, budget_s)
+        return cpu_baseline(N, C, S, budget_s, blocks)
     with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(N, C, S, budget_s)] * procs)
+        res = pool.map(_cpu_worker, [(N, C, S, budget_s, blocks)] * procs)
     total = sum(r["value"] for r in res)
     return {"value": total, "unit": "sims/s", "cores": procs, "kind": "port",
             "single_core_value": res[0]["value"],
@@ -181,8 +192,115 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
                          "a Winograd / implicit-GEMM dynamics conv per simulation"}
 
 
+PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def tower_roofline(N, C, blocks, G, sims, tower_ms, towers):
+    """Config 5's dominant kernel: k_tconv (one 3x3 conv of every active
+    leaf, bf16 MFMA).  Algorithmic FLOPs per launch = boards x 2 x N^2 x 9 x C^2
+    (the conv as the network defines it; the kernel also multiplies the
+    16-row tiles' pad rows: executed = boards x 2 x 16*ceil(N^2/16) x 9 x C^2),
+    over the average launch duration = the timed towers' event spans / the
+    2*blocks+1 launches of a tower (so the inter-launch gaps are included)."""
+    L = 2 * blocks + 1
+    avg_launch_s = tower_ms / 1e3 / max(towers, 1) / L
+    boards = sims / max(towers, 1)                       # leaves evaluated per tower (terminal leaves skip)
+    alg = boards * 2 * N * N * 9 * C * C
+    exe = boards * 2 * 16 * ((N * N + 15) // 16) * 9 * C * C
+    ach = alg / avg_launch_s / 1e12
+    out = {"bound": "mfma", "kernel": f"k_tconv<{N}>", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS,
+           "unit": "TFLOP/s", "frac": ach / PEAK_BF16_MFMA_TFLOPS, "traffic": None,
+           "avg_launch_ms": avg_launch_s * 1e3, "launches_per_simulation": L, "boards_per_launch": boards,
+           "flops_per_launch": alg, "executed_flops_per_launch": exe,
+           "mfma_executed_tflops": exe / avg_launch_s / 1e12,
+           "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board) / average k_tconv launch time "
+                   "(HIP events around each simulation's tower / its launches, gaps included)"}
+    path = os.path.join(ROOT, "profiles", "latest_tower_pmc.json")
+    if os.path.exists(path):
+        p = json.load(open(path))
+        if p.get("workload") == f"{N}x{N}/C{C}/B{blocks}/G{G}":
+            out["traffic"] = p.get("hbm_bytes_per_launch")
+            out["pmc_source"] = f"profiles/{p['tag']}_pmc.json"
+            out["pmc"] = p.get("derived")
+    return out
+
+
+def tower_main(args, world, rank, local, cpu_ref):
+    """BASELINE config 5: 19x19, 20-block residual nets (C=256), 1600
+    simulations per move, 64 games per GPU (mzgo.ResMuZeroNet on the tower
+    engine).  A step = one move of every game (1600 simulations each); whole
+    games (up to 361 moves) are out of a bench's time budget at this size."""
+    import mzgo
+    N, C, S, G, B = args.board_size, args.latent_dim, args.sims, args.games, args.blocks
+    A = N * N + 1
+    net = mzgo.ResMuZeroNet(C, A, B).to(f"cuda:{local}").eval()
+    if rank == 0:
+        net.load_state_dict(mzgo.deterministic_res_state_dict(C, A, B, 0))
+    if world > 1:
+        from mzgo import distributed as mdist
+        mdist.broadcast_weights(net)
+    sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G)
+    eng = sp.engine
+    sp.reset(epoch=0)
+    for _ in range(args.warmup):
+        sp.move()
+    torch.cuda.synchronize()
+    eng.tower_timing(True)
+    c0 = eng.counters()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sp.move()
+    if world > 1:
+        from mzgo import distributed as mdist
+        mdist.gather_packed(mdist.pack_engine(eng), to_host=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tower_ms, towers = eng.tower_timing(False)
+    c1 = eng.counters()
+    sims = c1["simulations"] - c0["simulations"]
+    moves = c1["moves"] - c0["moves"]
+    if world > 1:
+        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
+    if rank == 0:
+        workload = f"{N}x{N} Go self-play, {B}-block residual nets (C={C}), {G} parallel games/GPU, {S} sims/move"
+        roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers)
+        out = {
+            "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {B}-block residual "
+                      f"nets, {S} sims/move (BASELINE config 5)",
+            "value": sims / dt, "unit": "sims/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
+            "moves_per_s": moves / dt,
+            "config": {"workload": workload, "step": f"one move of {G} games/GPU ({S} simulations each; "
+                                                     f"{2 * B + 1} k_tconv launches per simulation)",
+                       "board_size": N, "latent_dim": C, "res_blocks": B, "games_per_gpu": G,
+                       "sims_per_move": S, "parallelism": f"game-sharded x{world}", "compat": "reference",
+                       "precision": "bf16 MFMA operands, fp32 accumulation, bf16 activations"},
+            "roofline": roof,
+        }
+        if cpu_ref is not None:
+            out["cpu_baseline"] = cpu_ref
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="2: 9x9 / 256 games / 200 sims (the headline, BASELINE configs[1]); "
+                         "5: 19x19 / 20-block residual nets / 1600 sims / 64 games (BASELINE configs[4])")
+    ap.add_argument("--blocks", type=int, default=20, help="residual blocks (config 5)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10, help="whole self-play epochs timed")
     ap.add_argument("--warmup", type=int, default=1, help="untimed epochs")
@@ -200,6 +318,13 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="oracle processes for cpu_baseline (the GPU box's CPU share is 16)")
     args = ap.parse_args()
+    if args.config == 5:
+        # config 5's sizes unless given explicitly
+        defaults = dict(board_size=9, games=256, sims=200, latent_dim=96, steps=10, warmup=1)
+        c5 = dict(board_size=19, games=64, sims=1600, latent_dim=256, steps=2, warmup=1)
+        for k, v in c5.items():
+            if getattr(args, k) == defaults[k]:
+                setattr(args, k, v)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -207,11 +332,15 @@ def main():
     cpu_ref = None
     if world == 1 and not args.no_cpu_baseline:
         # before the GPU is initialised: the baseline spawns worker processes
-        cpu_ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget, args.cpu_procs)
+        cpu_ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget, args.cpu_procs,
+                                     args.blocks if args.config == 5 else None)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.config == 5:
+        tower_main(args, world, rank, local, cpu_ref)
+        return
 
     import mzgo
 

@@ -162,6 +162,11 @@ int mzgo_arena_move(mzgo_engine* eng, mzgo_engine* opponent, void* stream);
 /* ``moves`` arena moves per slot in one launch (as mzgo_selfplay_moves). */
 int mzgo_arena_moves(mzgo_engine* eng, mzgo_engine* opponent, int moves, void* stream);
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
+/* Tower engines (tower = 1): report (synchronising) and reset the time spent
+ * in the dynamics towers since the last call -- one HIP event pair around each
+ * simulation step's 2*res_blocks+1 conv launches, on the launch stream -- then
+ * switch the timing on (enable = 1) or off. */
+int mzgo_tower_timing(mzgo_engine* eng, int enable, double* tower_ms_host, int64_t* towers_host);
 /* Test hook: use injected Dirichlet samples f64 [G][max_moves][A] (device,
  * caller-owned, must outlive the moves) instead of the counter-RNG sampler;
  * NULL restores sampling. */

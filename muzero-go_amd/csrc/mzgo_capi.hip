@@ -211,6 +211,7 @@ struct mzgo_engine {
   }
   ~mzgo_engine() {
     if (tower) {
+      for (hipEvent_t ev : tower->evs) (void)hipEventDestroy(ev);
       for (void* p : {tower->d_wb, (void*)tower->d_wf, (void*)tower->ib, (void*)tower->ob, (void*)tower->s0,
                       (void*)tower->s1, (void*)tower->shp, (void*)tower->sact})
         if (p) (void)hipFree(p);
@@ -707,6 +708,18 @@ int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* str
   pp.arena = 1;
   pp.moves = moves;
   HIPCHK(e->ks->selfplay_move(e->d_np, opponent->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_tower_timing(mzgo_engine* e, int enable, double* tower_ms, int64_t* towers) {
+  if (!e || !e->tower) return fail(MZGO_EINVAL, "not a tower engine");
+  TowerHost& t = *e->tower;
+  HIPCHK(t.harvest());
+  if (tower_ms) *tower_ms = t.tower_ms;
+  if (towers) *towers = t.towers_timed;
+  t.tower_ms = 0.0;
+  t.towers_timed = 0;
+  t.timing = enable != 0;
   return MZGO_OK;
 }
 

@@ -44,19 +44,56 @@ struct TGeo {
   static constexpr int CS = (CELLS + 15) / 16 * 16;     // head-partial row stride
   static constexpr int W = N + 2;                       // padded board side
   static constexpr int P = W * W;                       // padded pixels
-  static constexpr int PB = (P * 128 + 4095) / 4096 * 4096;   // LDS bytes of one 64-channel chunk
-  static constexpr int NPW = PB / 4096;                 // 1-KiB DMA pieces per wave per chunk
-  static constexpr int PST = NPW / 2;                   // steps over which the next chunk is fetched
   static constexpr int TT = (CELLS + 15) / 16;          // 16-pixel M tiles of a board
-  static constexpr int MT = (TT + 3) / 4;               // tiles per wave (4 waves)
-  static constexpr int WSLOT = 64 * 64 * 2;             // one (tap, cin chunk) weight tile
-  static constexpr int LDS = 2 * PB + 3 * WSLOT + 4 * 64 * 4;
   // tree kernels: one wave per game
   static constexpr int THREADS = 64, WAVES = 1, TREE_CAP = 0;
-  static_assert(PST <= 7, "a chunk's DMA must be issued within taps 0..6");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  static_assert(2 * PB >= CELLS * 272, "epilogue staging must fit the patch buffers");
 };
+
+// k_tconv geometry for NW waves per workgroup (one workgroup per CU).  The
+// k-loop runs in steps of one kernel row (3 taps x one 64-channel cin chunk):
+// a step's weight tile is 3 x 64 x 64 bf16 = 24 KiB.
+template <int N, int NW>
+struct TConvGeo {
+  typedef TGeo<N> G;
+  static constexpr int PBYTES = G::P * 128;             // one 64-channel chunk of the padded board
+  static constexpr int PPIECES = (PBYTES + 1023) / 1024;   // 1-KiB DMA pieces of a chunk (last one partial)
+  static constexpr int PB = (PBYTES + 15) / 16 * 16;    // its LDS buffer (the partial piece is masked)
+  static constexpr int NPW = (PPIECES + NW - 1) / NW;   // pieces of a chunk per wave (some waves one less)
+  static constexpr int WSLOT = 3 * 64 * 64 * 2;         // one step's weight tile
+  static constexpr int WPW = WSLOT / 1024 / NW;         // its 1-KiB pieces per wave
+  static constexpr int MT = (G::TT + NW - 1) / NW;      // 16-pixel tiles per wave
+  static constexpr int LDS = 2 * PB + 2 * WSLOT + 4 * 64 * 4;
+  static_assert(WPW * NW * 1024 == WSLOT, "whole weight pieces per wave");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(2 * PB >= G::CELLS * 272, "epilogue staging must fit the patch buffers");
+  // next chunk's patch pieces a wave issues at step ky (0, 1) of the current chunk
+  __device__ static int pieces_at(int ky, int wave) {
+    const int k0 = ky == 0 ? 0 : (NPW + 1) / 2, k1 = ky == 0 ? (NPW + 1) / 2 : NPW;
+    int n = 0;
+    for (int k = k0; k < k1; ++k) n += (k * NW + wave < PPIECES) ? 1 : 0;
+    return n;
+  }
+};
+
+// GEMM row m -> board cell (raster index), -1 for a pad row.  N >= 16: the
+// first 16 cells of every board row are rows 16y..16y+15 (a tile = 16
+// consecutive pixels of one board row: its A-fragment reads are bank-conflict
+// free, see frag_ld), the remaining columns follow column by column; smaller
+// boards in raster order.
+#ifndef MZGO_TOWER_ROWSEG
+#define MZGO_TOWER_ROWSEG 0
+#endif
+constexpr bool kTowerRowSegments = MZGO_TOWER_ROWSEG != 0;
+template <int N>
+__device__ __forceinline__ int tcell(int m) {
+  if constexpr (N >= 16 && kTowerRowSegments) {
+    if (m < 16 * N) return (m >> 4) * N + (m & 15);
+    const int r = m - 16 * N;
+    return r < N * (N - 16) ? (r % N) * N + 16 + r / N : -1;
+  } else {
+    return m < N * N ? m : -1;
+  }
+}
 
 // element offset of (padded pixel q, channel c) inside one 64-channel chunk
 __device__ __forceinline__ int tpix(int q, int piece) { return q * 64 + ((piece ^ ((q >> 1) & 7)) << 3); }
@@ -82,29 +119,51 @@ struct TConvArgs {
 template <class G, int T>
 struct TapOff { static constexpr int v = (T / 3) * G::W + (T % 3); };
 
-// s_waitcnt vmcnt for step (cc, t): the DMAs younger than weight tile W(s)
-// are the next chunk's pieces of steps s-2 and s-1 and W(s+1) (see k_tconv).
-template <class G, int T>
-__device__ __forceinline__ void tconv_wait(bool nextp, bool last) {
-  constexpr int p2 = (T >= 2 && T - 2 < G::PST) ? 2 : 0;
-  constexpr int p1 = (T >= 1 && T - 1 < G::PST) ? 2 : 0;
-  const int w1 = (last && T == 8) ? 0 : 2;
-  if (nextp) {
-    if (w1) wait_vmcnt<p2 + p1 + 2>(); else wait_vmcnt<p2 + p1>();
-  } else {
-    if (w1) wait_vmcnt<2>(); else wait_vmcnt<0>();
-  }
-}
-
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 }
 
-template <int N>
-__global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63]
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  switch (n) {
+#define MZGO_W(k) case k: wait_vmcnt<k>(); break;
+    MZGO_W(0) MZGO_W(1) MZGO_W(2) MZGO_W(3) MZGO_W(4) MZGO_W(5) MZGO_W(6) MZGO_W(7) MZGO_W(8) MZGO_W(9)
+    MZGO_W(10) MZGO_W(11) MZGO_W(12) MZGO_W(13) MZGO_W(14) MZGO_W(15) MZGO_W(16) MZGO_W(17) MZGO_W(18)
+    MZGO_W(19) MZGO_W(20) MZGO_W(21) MZGO_W(22) MZGO_W(23) MZGO_W(24) MZGO_W(25) MZGO_W(26) MZGO_W(27)
+    MZGO_W(28) MZGO_W(29) MZGO_W(30) MZGO_W(31)
+#undef MZGO_W
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
+#ifdef MZGO_TCONV_STAMPS
+// diagnostic build: per-workgroup cycle sums (wave 0): 0 total, 1 prologue,
+// 2 vmcnt waits, 3 barriers, 4 MFMA steps, 5 epilogue, 6 launches
+__device__ unsigned long long g_tstamps[4096][8];
+#endif
+
+// 16 bytes of an MFMA fragment (one ds_read_b128).  (Two ds_read_b64 with
+// the halves of odd k-groups swapped on both operands are bank-conflict free
+// for 16 consecutive pixel rows, but measured 1.6x slower: b64 reads need
+// more waves per SIMD than this kernel has.)
+__device__ __forceinline__ bf16x8 frag_ld(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+#ifdef MZGO_TCONV_STAMPS
+#define STAMP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define STAMP_T(v) do {} while (0)
+#endif
+
+template <int N, int NW>
+__global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
   typedef TGeo<N> G;
-  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
+  typedef TConvGeo<N, NW> T;
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+  STAMP_T(tstart);
+#ifdef MZGO_TCONV_STAMPS
+  unsigned long long acc_wait = 0, acc_bar = 0, acc_mfma = 0;
+#endif
   const int CO = a.co_chunks, CC = a.ci_chunks;
   // block -> (board, cout chunk); a board's chunks on one XCD (blocks b, b+8,
   // ... share one under round-robin dispatch: speed only) when the grid allows
@@ -122,8 +181,8 @@ __global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* const patch0 = lds;
-  char* const wring = lds + 2 * G::PB;
-  float* const sbias = reinterpret_cast<float*>(lds + 2 * G::PB + 3 * G::WSLOT);
+  char* const wring = lds + 2 * T::PB;
+  float* const sbias = reinterpret_cast<float*>(lds + 2 * T::PB + 2 * T::WSLOT);
   float* const shw = sbias + 64;
   const bf16* in = a.in + (long long)(a.in_idx ? a.in_idx[b] : b) * a.in_stride;
   const bf16* wsrc = a.w + (size_t)cg * CC * 9 * 64 * 64;
@@ -134,36 +193,42 @@ __global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA counts below start from zero
 
-  // DMA issue helpers (16 B per lane; the LDS destination is base + lane*16)
+  // DMA issue helpers (16 B per lane; the LDS destination is base + lane*16).
+  // Step s = 3*cc + ky: weight tile W(s) = taps 3ky..3ky+2 of cin chunk cc,
+  // ring slot s % 2.  After step s's barrier every wave issues its pieces of
+  // W(s+1) and, at ky = 0 and 1, of the next chunk's patch (other buffer);
+  // before step s it waits for W(s): the only DMAs younger than W(s) are the
+  // patch pieces of step s-1.  A chunk's patch is issued at steps ky 0 and 1
+  // of the previous chunk, before W(its first step): the same wait covers it.
   auto issue_patch_pieces = [&](int cc, int buf, int k0, int k1) {
     const char* src = reinterpret_cast<const char*>(in + (size_t)cc * G::P * 64);
     for (int k = k0; k < k1; ++k) {
-      const int ii = k * 4 + wave;                       // 1-KiB piece of the chunk
-      const int piece = ii * 64 + lane;                  // 16-B piece
-      const char* g = src + (piece * 16 < G::P * 128 ? piece * 16 : 0);
-      dma16(g, lds_addr(patch0 + buf * G::PB + ii * 1024));
+      const int ii = k * NW + wave;                      // 1-KiB piece of the chunk
+      if (ii >= T::PPIECES) break;                       // wave-uniform
+      const int off = ii * 1024 + lane * 16;
+      if (off < T::PBYTES)                               // the last piece is partial
+        dma16(src + off, lds_addr(patch0 + buf * T::PB + ii * 1024));
     }
   };
   auto issue_w = [&](int s) {
-    const char* src = reinterpret_cast<const char*>(wsrc + (size_t)s * 64 * 64);
-    char* slot = wring + (s % 3) * G::WSLOT;
+    const char* src = reinterpret_cast<const char*>(wsrc + (size_t)s * 3 * 64 * 64);
+    char* slot = wring + (s & 1) * T::WSLOT;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int ii = k * 4 + wave;
+    for (int k = 0; k < T::WPW; ++k) {
+      const int ii = k * NW + wave;
       dma16(src + ii * 1024 + lane * 16, lds_addr(slot + ii * 1024));
     }
   };
-  const int total = 9 * CC;
-  issue_patch_pieces(0, 0, 0, G::NPW);
+  const int nsteps = 3 * CC;
+  issue_patch_pieces(0, 0, 0, T::NPW);
   issue_w(0);
-  if (total > 1) issue_w(1);
 
-  // per-lane A-fragment pixel bases (pixel p = tile*16 + (lane & 15))
-  int qb[G::MT];
+  // per-lane A-fragment pixel bases (cell of GEMM row tile*16 + (lane & 15))
+  int qb[T::MT];
 #pragma unroll
-  for (int i = 0; i < G::MT; ++i) {
-    const int p = (wave * G::MT + i) * 16 + (lane & 15);
-    qb[i] = p < G::CELLS ? (p / N) * G::W + (p % N) : 0;
+  for (int i = 0; i < T::MT; ++i) {
+    const int p = tcell<N>((wave * T::MT + i) * 16 + (lane & 15));
+    qb[i] = p >= 0 ? (p / N) * G::W + (p % N) : 0;
   }
   // per-lane B-fragment byte offsets (cout row n*16 + (lane & 15), piece lane >> 4)
   int boff[4];
@@ -172,67 +237,80 @@ __global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
     const int r = n * 16 + (lane & 15);
     boff[n] = r * 128 + (((lane >> 4) ^ ((r >> 1) & 7)) << 4);
   }
-  f32x4 acc[G::MT][4];
+  f32x4 acc[T::MT][4];
 #pragma unroll
-  for (int i = 0; i < G::MT; ++i)
+  for (int i = 0; i < T::MT; ++i)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  STAMP_T(tpro);
 
   for (int cc = 0; cc < CC; ++cc) {
-    const bool nextp = cc + 1 < CC, last = !nextp;
-    const char* pbuf = patch0 + (cc & 1) * G::PB;
-    auto step = [&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      const int s = cc * 9 + t;
-      tconv_wait<G, t>(nextp, last);
+    const bool nextp = cc + 1 < CC;
+    const char* pbuf = patch0 + (cc & 1) * T::PB;
+    auto step = [&](auto kyc) {
+      constexpr int ky = decltype(kyc)::value;
+      const int s = cc * 3 + ky;
+      STAMP_T(ts0);
+      // younger than W(s): the patch pieces of step s-1 (ky-1 of this chunk)
+      int younger = 0;
+      if (ky >= 1 && ky - 1 < 2 && nextp) younger = T::pieces_at(ky - 1, wave);
+      wait_vmcnt_dyn(younger);
+      STAMP_T(ts1);
       lds_barrier();                                   // W(s) (and chunk cc) landed for every wave
-      if (s + 2 < total) issue_w(s + 2);
-      if (nextp && t < G::PST) issue_patch_pieces(cc + 1, (cc + 1) & 1, 2 * t, 2 * t + 2);
-      const char* ws = wring + (t % 3) * G::WSLOT;
-      bf16x8 bf[4][2];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        bf[n][0] = *reinterpret_cast<const bf16x8*>(ws + boff[n]);
-        bf[n][1] = *reinterpret_cast<const bf16x8*>(ws + (boff[n] ^ 64));
+      STAMP_T(ts2);
+      if (s + 1 < nsteps) issue_w(s + 1);
+      if (nextp && ky < 2) {
+        constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
+        issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
       }
+      const char* ws = wring + (s & 1) * T::WSLOT;
 #pragma unroll
-      for (int i = 0; i < G::MT; ++i) {
-        if (wave * G::MT + i >= G::TT) break;          // wave-uniform
-        const int q = qb[i] + TapOff<G, t>::v;
-        const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(pbuf + off);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(pbuf + (off ^ 64));
+      for (int kx = 0; kx < 3; ++kx) {
+        const char* wt = ws + kx * 64 * 64 * 2;
+        bf16x8 bf[4][2];
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[n][0], acc[i][n], 0, 0, 0);
-          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[n][1], acc[i][n], 0, 0, 0);
+          bf[n][0] = frag_ld(wt + boff[n]);
+          bf[n][1] = frag_ld(wt + (boff[n] ^ 64));
+        }
+#pragma unroll
+        for (int i = 0; i < T::MT; ++i) {
+          if (wave * T::MT + i >= G::TT) break;        // wave-uniform
+          const int q = qb[i] + ky * G::W + kx;
+          const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
+          const bf16x8 a0 = frag_ld(pbuf + off);
+          const bf16x8 a1 = frag_ld(pbuf + (off ^ 64));
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[n][0], acc[i][n], 0, 0, 0);
+            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[n][1], acc[i][n], 0, 0, 0);
+          }
         }
       }
+      STAMP_T(ts3);
+#ifdef MZGO_TCONV_STAMPS
+      acc_wait += ts1 - ts0; acc_bar += ts2 - ts1; acc_mfma += ts3 - ts2;
+#endif
     };
     step(std::integral_constant<int, 0>{});
     step(std::integral_constant<int, 1>{});
     step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{});
-    step(std::integral_constant<int, 4>{});
-    step(std::integral_constant<int, 5>{});
-    step(std::integral_constant<int, 6>{});
-    step(std::integral_constant<int, 7>{});
-    step(std::integral_constant<int, 8>{});
   }
   lds_barrier();                                       // every wave's last reads done
+  STAMP_T(tloop);
 
   // epilogue 1: accumulators -> fp32 staging [cell][68] (over the patch buffers)
   float* st = reinterpret_cast<float*>(lds);
 #pragma unroll
-  for (int i = 0; i < G::MT; ++i) {
-    const int ti = wave * G::MT + i;
+  for (int i = 0; i < T::MT; ++i) {
+    const int ti = wave * T::MT + i;
     if (ti >= G::TT) break;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = ti * 16 + (lane >> 4) * 4 + r;
-        if (p < G::CELLS) st[p * 68 + n * 16 + (lane & 15)] = acc[i][n][r];
+        const int p = tcell<N>(ti * 16 + (lane >> 4) * 4 + r);
+        if (p >= 0) st[p * 68 + n * 16 + (lane & 15)] = acc[i][n][r];
       }
   }
   __syncthreads();
@@ -241,7 +319,7 @@ __global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
   const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
                           : nullptr;
   const float* et = a.etab ? a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64 : nullptr;
-  for (int idx = tid; idx < G::CELLS * 8; idx += 256) {
+  for (int idx = tid; idx < G::CELLS * 8; idx += 64 * NW) {
     const int p = idx >> 3, j = idx & 7;
     const int y = p / N, x = p - y * N;
     const int q = (y + 1) * G::W + (x + 1);
@@ -287,6 +365,14 @@ __global__ void __launch_bounds__(256) k_tconv(TConvArgs a) {
       }
     }
   }
+#ifdef MZGO_TCONV_STAMPS
+  if (tid == 0 && bid < 4096) {
+    const unsigned long long tend = __builtin_amdgcn_s_memtime();
+    unsigned long long* g = g_tstamps[bid];
+    g[0] += tend - tstart; g[1] += tpro - tstart; g[2] += acc_wait; g[3] += acc_bar; g[4] += acc_mfma;
+    g[5] += tend - tloop; g[6] += 1;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------

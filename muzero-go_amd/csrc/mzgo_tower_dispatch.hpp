@@ -1,6 +1,8 @@
 // mzgo_tower_dispatch.hpp -- host launchers of the residual-tower engine
 // (mzgo_tower.hpp) for one board size, gathered in a table.
 #pragma once
+#include <cstdlib>
+
 #include "mzgo_tower.hpp"
 
 namespace mzgo {
@@ -29,11 +31,19 @@ struct TowerSet {
 };
 
 const TowerSet* find_tower(int N);
+#ifdef MZGO_TCONV_STAMPS
+int tower_stamps_n19(unsigned long long* out);
+#endif
 
 template <int N>
 struct TLaunch {
   static hipError_t conv(const TConvArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((k_tconv<N>), dim3(a.nboards * a.co_chunks), dim3(256), 0, s, a);
+    // 8 waves (2 per SIMD) unless MZGO_TCONV_WAVES=4 (A/B runs)
+    static const int nw = [] { const char* e = getenv("MZGO_TCONV_WAVES"); return e && atoi(e) == 4 ? 4 : 8; }();
+    if (nw == 4)
+      hipLaunchKernelGGL((k_tconv<N, 4>), dim3(a.nboards * a.co_chunks), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_tconv<N, 8>), dim3(a.nboards * a.co_chunks), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   static hipError_t obs(const TowerArrays& T, const SearchParams& sp, const PlayParams& pp, const EngineArrays& E,

@@ -64,7 +64,39 @@ struct TowerHost {
   const float* etab = nullptr;
   HeadScalars hs{};
 
+  // optional timing of the dynamics towers (bench.py --config 5): one event
+  // pair around each simulation step's tower, on the launch stream
+  bool timing = false;
+  std::vector<hipEvent_t> evs;
+  size_t ev_used = 0;
+  long long towers_timed = 0;
+  double tower_ms = 0.0;
+
   long long slot() const { return (long long)CC * P * 64; }
+
+  hipError_t mark(hipStream_t s) {
+    if (!timing) return hipSuccess;
+    if (ev_used == evs.size()) {
+      hipEvent_t e;
+      hipError_t r = hipEventCreate(&e);
+      if (r != hipSuccess) return r;
+      evs.push_back(e);
+    }
+    return hipEventRecord(evs[ev_used++], s);
+  }
+  // sum the recorded spans (synchronises) and recycle the events
+  hipError_t harvest() {
+    for (size_t i = 0; i + 1 < ev_used; i += 2) {
+      hipError_t r = hipEventSynchronize(evs[i + 1]);
+      if (r != hipSuccess) return r;
+      float ms = 0.f;
+      if ((r = hipEventElapsedTime(&ms, evs[i], evs[i + 1])) != hipSuccess) return r;
+      tower_ms += ms;
+      towers_timed += 1;
+    }
+    ev_used = 0;
+    return hipSuccess;
+  }
 
   static std::vector<std::pair<std::string, std::vector<int64_t>>> specs(int C, int A, int blocks) {
     std::vector<std::pair<std::string, std::vector<int64_t>>> s;
@@ -228,15 +260,18 @@ struct TowerHost {
   }
 
   // S simulations: select (all games) -> dynamics tower (all leaves) -> expand + backup
-  hipError_t simulations(const SearchParams& sp, const EngineArrays& E, hipStream_t s) const {
+  hipError_t simulations(const SearchParams& sp, const EngineArrays& E, hipStream_t s) {
     hipError_t e;
     for (int i = 0; i < S; ++i) {
       if ((e = ts->select(TA, sp, E, G, s)) != hipSuccess) return e;
+      if ((e = mark(s)) != hipSuccess) return e;
       if ((e = tower(dyn, TA.pool, TA.in_idx, slot(), TA.pool, TA.out_idx, slot(), TA.act, TA.evalact, G, t0, t1,
                      TA.hpart, s)) != hipSuccess)
         return e;
+      if ((e = mark(s)) != hipSuccess) return e;
       if ((e = ts->expand(TA, sp, E, G, s)) != hipSuccess) return e;
     }
+    if (timing) return harvest();
     return hipSuccess;
   }
 };

@@ -213,6 +213,14 @@ class Engine:
         self._noise = noise      # keep it alive while moves use it
         check(lib.mzgo_selfplay_inject_noise(self._h, ptr(noise)))
 
+    def tower_timing(self, enable):
+        """Tower engines: (ms, towers) spent in dynamics towers since the last
+        call (synchronises), then timing on/off (mzgo_tower_timing)."""
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(lib.mzgo_tower_timing(self._h, int(enable), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
     def counters(self):
         out = np.zeros(5, np.uint64)
         check(lib.mzgo_selfplay_counters(self._h, ptr(out), stream_of(self.device)))

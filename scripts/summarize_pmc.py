@@ -19,6 +19,7 @@ workload = sys.argv[2] if len(sys.argv) > 2 else "9x9 Go self-play, 256 parallel
 dynamics = sys.argv[3] if len(sys.argv) > 3 else "factored"
 kernel = sys.argv[4] if len(sys.argv) > 4 else "k_selfplay_move"
 moves_per_launch = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # bench.py --moves-per-launch (0: whole games)
+latest = sys.argv[6] if len(sys.argv) > 6 else "latest_pmc.json"       # the file bench.py reads
 src = os.path.join("gpurun_out", f"pmc_{tag}")
 os.makedirs("profiles", exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join("profiles", f"{tag}_kernel_stats.csv"))
@@ -54,6 +55,7 @@ if "GRBM_GUI_ACTIVE" in c:
         "effective_clock_GHz": clk / 1e9,
         "valu_issue_frac": c.get("SQ_INSTS_VALU", 0) / (2 * cu_cycles),
         "mfma_busy_frac": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (4 * cu_cycles),
+        "mfma_insts_per_launch": c.get("SQ_INSTS_MFMA", 0),
         "lds_array_busy_frac": c.get("SQ_LDS_IDX_ACTIVE", 0) / cu_cycles,
         "lds_bank_conflict_share": c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1.0, c.get("SQ_LDS_IDX_ACTIVE", 0)),
         "wave_wait_any_share": c.get("SQ_WAIT_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
@@ -64,5 +66,5 @@ if "GRBM_GUI_ACTIVE" in c:
                 "wave shares of SQ_WAVE_CYCLES (quad-cycles, as the SQ_WAIT_*/ACTIVE_* counters)",
     }
 json.dump(out, open(os.path.join("profiles", f"{tag}_pmc.json"), "w"), indent=1)
-json.dump(out, open(os.path.join("profiles", "latest_pmc.json"), "w"), indent=1)
+json.dump(out, open(os.path.join("profiles", latest), "w"), indent=1)
 print(json.dumps(out, indent=1))
