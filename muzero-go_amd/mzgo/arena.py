@@ -15,6 +15,7 @@ ended); the Elo update is :603-606.  Randomness: counter streams keyed by
 (seed, game id, move) as everywhere in the engine (not Python's RNG).
 """
 import numpy as np
+import torch
 
 from .selfplay import history_from_device
 
@@ -44,12 +45,18 @@ class SelfPlayEvaluator:
                         dirichlet_epsilon=dirichlet_epsilon, pass_epsilon=pass_epsilon, discount=discount,
                         max_moves=self.max_moves, komi=float(komi), seed=seed)
 
-    def play(self):
-        """Play all games; returns the per-game winner (+1 black, -1 white, 0)."""
+    def play(self, noise=None):
+        """Play all games; returns the per-game winner (+1 black, -1 white, 0).
+        noise: test hook, Dirichlet samples float64 [num_games, max_moves, A]
+        in place of the counter-RNG draws (Engine.inject_noise)."""
         eng = self.current.engine(self.num_games, self.S, **self.cfg)
         opp = self.best.engine(self.num_games, self.S, **self.cfg)
+        eng.inject_noise(noise)
         eng.selfplay_reset(self.epoch)
         eng.arena_move(opp, self.max_moves)          # whole games, one launch
+        if noise is not None:
+            torch.cuda.synchronize(eng.device)       # the launch reads the samples until it ends
+            eng.inject_noise(None)
         self.epoch += 1
         N = self.current.board_size
         return np.array([float(history_from_device(eng.record(g), N, self.discount).final_reward)

@@ -18,14 +18,19 @@ on the device, every game of a batch at once) and trains on it:
   batch's mean loss; ``StepLR`` stepped once per batch.  Pinned by a step
   recorded from the reference (``tests/golden/train_*``).
 * ``mode="batched"`` -- the same losses for all B trajectories in one unroll
-  (B x 10 recurrent steps per launch) and ONE optimizer step on their summed
-  gradient; the bootstrap values of every (trajectory, unroll step) pair come
-  from one batched ``initial_inference`` on the HIP engine.
+  (B x 10 recurrent steps, each one launch for all B) and ONE optimizer step
+  on their summed gradient; the bootstrap values of every (trajectory, unroll
+  step) pair come from one batched ``initial_inference`` on the HIP engine.
+  On the GPU the unroll's forward runs on the HIP kernels
+  (``initial_inference_hip`` / ``recurrent_inference_hip``: the engine's
+  k_initial_inference / k_recurrent_inference for the 3x3 convs, autograd
+  Functions whose backward is torch's -- from the saved input and output for
+  the dynamics conv, by recomputing the representation's hidden activations);
+  the 1x1 heads stay torch ops on the engine's latents.
 
-The network's differentiable forward (``initial_inference_torch`` /
-``recurrent_inference_torch``) restates main.py:72-144 with torch ops on the
-module's own parameters (autograd needs them); the HIP kernels are
-inference-only.  Replay buffers restate main.py:158-244.
+``initial_inference_torch`` / ``recurrent_inference_torch`` restate
+main.py:72-144 with torch ops on the module's own parameters (reference
+mode, and the CPU).  Replay buffers restate main.py:158-244.
 """
 import random
 from dataclasses import dataclass
@@ -86,6 +91,75 @@ def recurrent_inference_torch(net, latent, action):
     b = latent.shape[0]
     emb = d.action_embedding(action).view(b, latent.shape[1], 1, 1).expand_as(latent)
     x = F.relu(d.conv(latent + emb))
+    reward = d.fc_reward_output(F.relu(d.fc_reward_hidden(d.reward_conv(x).mean(dim=[2, 3]))))
+    value, logits = _prediction(net, x)
+    return x, reward, value, logits
+
+
+# ---------------------------------------------------------------------------
+# the same networks with the forward on the HIP engine (SURVEY.md §8(f) 1:
+# "forward only through HIP, backward via torch")
+# ---------------------------------------------------------------------------
+class _HipDynamicsConv(torch.autograd.Function):
+    """x' = relu(conv3x3(latent + emb[a]) + b) (main.py:97-103) with the
+    forward on the engine's k_recurrent_inference; the backward in torch from
+    the saved input and output (ReLU mask = x' > 0; conv2d_input /
+    conv2d_weight; the embedding's gradient = the input gradient summed over
+    the board, added into row a)."""
+
+    @staticmethod
+    def forward(ctx, latent, action, weight, bias, emb, net):
+        nxt, _, _, _ = net.engine().recurrent_inference(latent.detach(), action)
+        ctx.save_for_backward(latent, action, weight, emb, nxt)
+        return nxt
+
+    @staticmethod
+    def backward(ctx, g):
+        latent, action, weight, emb, nxt = ctx.saved_tensors
+        gp = g * (nxt > 0).to(g.dtype)
+        x = latent + emb[action][:, :, None, None]
+        gx = torch.nn.grad.conv2d_input(x.shape, weight, gp, padding=1)
+        gw = torch.nn.grad.conv2d_weight(x, weight.shape, gp, padding=1)
+        gb = gp.sum(dim=(0, 2, 3))
+        gemb = torch.zeros_like(emb).index_add_(0, action, gx.sum(dim=(2, 3)))
+        return gx, None, gw, gb, gemb, None
+
+
+class _HipRepresentation(torch.autograd.Function):
+    """The representation (main.py:72-84) with the forward on the engine's
+    k_initial_inference; the backward recomputes its two hidden activations
+    with torch (activation recomputation) and differentiates the torch graph."""
+
+    @staticmethod
+    def forward(ctx, obs, w1, b1, w2, b2, w3, b3, net):
+        lat, _, _ = net.engine().initial_inference(obs.detach())
+        ctx.save_for_backward(obs, w1, b1, w2, b2, w3, b3)
+        return lat
+
+    @staticmethod
+    def backward(ctx, g):
+        obs, *params = ctx.saved_tensors
+        with torch.enable_grad():
+            ps = [p.detach().requires_grad_(True) for p in params]
+            x = F.relu(F.conv2d(obs, ps[0], ps[1], padding=1))
+            x = F.relu(F.conv2d(x, ps[2], ps[3], padding=1))
+            lat = F.relu(F.conv2d(x, ps[4], ps[5], padding=1))
+            grads = torch.autograd.grad(lat, ps, g)
+        return (None, *grads, None)
+
+
+def initial_inference_hip(net, observation):
+    r = net.representation
+    latent = _HipRepresentation.apply(observation.contiguous(), r.conv1.weight, r.conv1.bias, r.conv2.weight,
+                                      r.conv2.bias, r.conv3.weight, r.conv3.bias, net)
+    value, logits = _prediction(net, latent)
+    return latent, value, logits
+
+
+def recurrent_inference_hip(net, latent, action):
+    d = net.dynamics
+    x = _HipDynamicsConv.apply(latent.contiguous(), action.contiguous(), d.conv.weight, d.conv.bias,
+                               d.action_embedding.weight, net)
     reward = d.fc_reward_output(F.relu(d.fc_reward_hidden(d.reward_conv(x).mean(dim=[2, 3]))))
     value, logits = _prediction(net, x)
     return x, reward, value, logits
@@ -240,10 +314,13 @@ class MuZeroTrainer:
     ``start_index(trajectory_length)`` draws a trajectory's start (main.py:395
     ``random.randint(0, T - 1)``; tests pass a fixed sequence)."""
 
-    def __init__(self, net: MuZeroNet, config: TrainConfig = None, mode="reference", start_index=None):
+    def __init__(self, net: MuZeroNet, config: TrainConfig = None, mode="reference", start_index=None,
+                 hip_forward=None):
         if mode not in ("reference", "batched"):
             raise ValueError(f"mode must be 'reference' or 'batched', not {mode!r}")
         self.net = net
+        # batched mode on the GPU: the unroll's forward on the HIP kernels
+        self.hip_forward = (next(net.parameters()).device.type == "cuda") if hip_forward is None else hip_forward
         self.config = config or TrainConfig()
         self.mode = mode
         self.action_size = net.board_size ** 2 + 1
@@ -388,7 +465,9 @@ class MuZeroTrainer:
         t_val, t_rew, t_pol = f32(t_val), f32(t_rew), f32(t_pol)
         obs0 = f32(np.stack([np.asarray(tr["observations"][s]) for tr, s in zip(batch, starts)]))
         self.optimizer.zero_grad()
-        latent, value, logits = initial_inference_torch(net, obs0)
+        fwd0, fwd = ((initial_inference_hip, recurrent_inference_hip) if self.hip_forward
+                     else (initial_inference_torch, recurrent_inference_torch))
+        latent, value, logits = fwd0(net, obs0)
         kl = lambda lg, tp: F.kl_div(F.log_softmax(lg, dim=1), tp, reduction="none").sum(dim=1)
         v_l = c.value_loss_weight * self._value_loss(value.squeeze(1), t_val[:, 0])
         p_l = c.policy_loss_weight * kl(logits, t_pol[:, 0])
@@ -396,7 +475,7 @@ class MuZeroTrainer:
         tot_v, tot_p, tot_r = v_l.sum().item(), p_l.sum().item(), 0.0
         acts_t = torch.as_tensor(acts, device=dev)
         for k in range(1, K + 1):
-            latent, reward, value, logits = recurrent_inference_torch(net, latent, acts_t[:, k - 1])
+            latent, reward, value, logits = fwd(net, latent, acts_t[:, k - 1])
             r_l = c.reward_loss_weight * F.mse_loss(reward.squeeze(1), t_rew[:, k - 1], reduction="none")
             v_l = c.value_loss_weight * self._value_loss(value.squeeze(1), t_val[:, k])
             p_l = c.policy_loss_weight * kl(logits, t_pol[:, k])

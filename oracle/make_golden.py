@@ -24,6 +24,8 @@ Fixtures:
   train_5x5_c32.npz    main.py's MuZeroAgent.train (main.py:381-522), two
                        batches on synthetic trajectories with fixed start
                        indices: losses, priorities, lr, final weights
+  arena_5x5_s16.npz    main.py's SelfPlayEvaluator (main.py:526-611) games
+                       between two networks under the same hooks
 Usage:  python -m oracle.make_golden   (from the repo root)
 """
 import json
@@ -400,6 +402,111 @@ def main():
     make_train(mn)
 
 
+def make_arena(mn, N=5, S=16, G=4, C=96, seed=21, seeds=(3, 4)):
+    """main.py's SelfPlayEvaluator (main.py:526-611): G games between two
+    main.py MuZeroNets (deterministic weights, seeds[0] = current,
+    seeds[1] = best) on oracle.goenv.GoEnv, game i started by the current
+    agent iff i is even (evaluate, :597-600).  Hooks per (game i, move m):
+    MCTS's random.choice -> TAG_SELECT draw of the simulation, the Dirichlet
+    draw -> injected_noise(seed, i, m), the evaluator's random.choice(valid
+    actions) -> TAG_ACTION draw (SearchHooks.action_index).  Records every
+    game's actions, env.winner(), play_game's result, and evaluate's win
+    rate and Elo."""
+    from oracle.goenv import GoEnv
+    from oracle.rng import SearchHooks, injected_noise
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    mn.config.board_size = N
+    mn.config.max_action_size = A
+    mn.config.max_game_moves = int(N * N * 1.5)
+
+    class _Agent:
+        def __init__(self, s):
+            self.net = mn.MuZeroNet(C, A)
+            self.net.load_state_dict({k: torch.from_numpy(v) for k, v in deterministic_state_dict(C, A, s).items()})
+            self.net.eval()
+            self.action_size = A
+            self.mcts_simulations = S
+
+    cur, best = _Agent(seeds[0]), _Agent(seeds[1])
+    st = {"game": 0, "move": 0, "sim": -1, "in_search": False, "hooks": None}
+    saved = (mn.random.choice, mn.apply_dirichlet_noise, mn.MCTS.select_leaf, mn.MCTS.run)
+    orig_select, orig_run = mn.MCTS.select_leaf, mn.MCTS.run
+
+    def run(self_, obs):
+        st["hooks"] = SearchHooks(seed, st["game"], st["move"])
+        st["sim"], st["in_search"] = -1, True
+        try:
+            return orig_run(self_, obs)
+        finally:
+            st["in_search"] = False
+            st["move"] += 1
+
+    def select_leaf(self_, node):
+        st["sim"] += 1
+        return orig_select(self_, node)
+
+    def choice(seq):
+        h = st["hooks"]
+        if st["in_search"]:
+            return seq[h.choice_index(len(seq), st["sim"])]
+        # the evaluator's fallback, drawn for the move just searched
+        return seq[SearchHooks(seed, st["game"], st["move"] - 1).action_index(len(seq))]
+
+    def noise(policy, alpha, epsilon):
+        return (1 - epsilon) * policy + epsilon * injected_noise(seed, st["game"], st["move"], len(policy))
+    mn.random.choice, mn.apply_dirichlet_noise = choice, noise
+    mn.MCTS.select_leaf, mn.MCTS.run = select_leaf, run
+    env = GoEnv(N)
+    ev = mn.SelfPlayEvaluator(cur, best, env, num_games=G)
+    actions, winners, results = [], [], []
+    orig_step = env.step
+    try:
+        for i in range(G):
+            st["game"], st["move"] = i, 0
+            acts = []
+
+            def step(a, _acts=acts):
+                _acts.append(int(a))
+                return orig_step(a)
+            env.step = step
+            with torch.no_grad():
+                results.append(ev.play_game(starting_player=i % 2))
+            winners.append(float(env.winner()))
+            actions.append(acts)
+        # evaluate()'s scoring of the same games (:597-611)
+        wins = sum((1 - r) if i % 2 == 1 else r for i, r in enumerate(results))
+        win_rate = wins / G
+        expected = 1 / (1 + 10 ** ((ev.best_elo - ev.current_elo) / 400))
+        elo = ev.current_elo
+        if win_rate > mn.config.evaluation_win_threshold:
+            elo = ev.current_elo + mn.config.elo_k * (win_rate - expected)
+    finally:
+        mn.random.choice, mn.apply_dirichlet_noise, mn.MCTS.select_leaf, mn.MCTS.run = saved
+        env.step = orig_step
+    L = max(len(a) for a in actions)
+    pad = np.full((G, L), -1, np.int64)
+    for i, a in enumerate(actions):
+        pad[i, :len(a)] = a
+    out = dict(actions=pad, lengths=np.array([len(a) for a in actions], np.int64),
+               winners=np.array(winners, np.float64), results=np.array(results, np.int64),
+               win_rate=np.float64(win_rate), elo=np.float64(elo), initial_elo=np.float64(mn.config.initial_elo),
+               seed=np.int64(seed), seeds=np.array(seeds, np.int64), N=np.int64(N), S=np.int64(S),
+               G=np.int64(G), C=np.int64(C), max_moves=np.int64(mn.config.max_game_moves))
+    np.savez_compressed(os.path.join(GOLDEN, f"arena_{N}x{N}_s{S}.npz"), **out)
+    print("arena", N, "lengths", out["lengths"], "winners", winners, "results", results, "win_rate", win_rate)
+
+
+def arena_only():
+    """Regenerate only the arena fixture (``python -m oracle.make_golden arena``)."""
+    os.makedirs(GOLDEN, exist_ok=True)
+    sys.path.insert(0, REPO)
+    import_reference()
+    torch.set_num_threads(1)
+    import main as mn  # noqa: E402
+    make_arena(mn)
+
+
 def train_only():
     """Regenerate only the trainer fixture (``python -m oracle.make_golden train``)."""
     os.makedirs(GOLDEN, exist_ok=True)
@@ -423,4 +530,4 @@ def main_only():
 
 
 if __name__ == "__main__":
-    {"main": main_only, "train": train_only}.get(sys.argv[1] if sys.argv[1:] else "", main)()
+    {"main": main_only, "train": train_only, "arena": arena_only}.get(sys.argv[1] if sys.argv[1:] else "", main)()

@@ -62,3 +62,33 @@ def test_arena_first_mover_alternates_by_game():
         for g in range(G):
             if g % 2 == parity:
                 np.testing.assert_array_equal(first[g], e1.record(g)["policy"][0])
+
+
+@pytest.mark.gpu
+def test_arena_matches_reference_evaluator(golden_dir):
+    """Games recorded from the reference SelfPlayEvaluator (main.py:526-611,
+    tests/golden/arena_5x5_s16.npz; oracle/make_golden.py make_arena) under
+    the counter-stream hooks: the device arena plays the same moves in every
+    game, reaches the same winners and the same win rate / Elo update."""
+    from oracle.rng import injected_noise
+    g = np.load(f"{golden_dir}/arena_5x5_s16.npz")
+    N, S, G, C, seed = (int(g[k]) for k in ("N", "S", "G", "C", "seed"))
+    A = N * N + 1
+    cur, best = _nets(N, C, [int(x) for x in g["seeds"]])
+    ev = SelfPlayEvaluator(cur, best, num_games=G, num_simulations=S, seed=seed)
+    assert ev.max_moves == int(g["max_moves"])
+    noise = np.stack([[injected_noise(seed, i, m, A) for m in range(ev.max_moves)] for i in range(G)])
+    winners = ev.play(noise=noise)
+    torch.cuda.synchronize()
+    eng = cur.engine(G, S, **ev.cfg)
+    for i in range(G):
+        L = int(g["lengths"][i])
+        rec = eng.record(i)
+        assert rec["length"] == L, (i, rec["length"], L)
+        np.testing.assert_array_equal(rec["action"], g["actions"][i, :L], err_msg=f"game {i}")
+    np.testing.assert_array_equal(winners, g["winners"])
+    wr = SelfPlayEvaluator.win_rate(winners)
+    assert wr == float(g["win_rate"])
+    expected = 1 / (1 + 10 ** ((ev.best_elo - ev.current_elo) / 400))
+    elo = ev.current_elo + (ev.elo_k * (wr - expected) if wr > ev.win_threshold else 0.0)
+    assert elo == float(g["elo"])

@@ -103,3 +103,53 @@ def test_batched_mode_trains_on_selfplay_output():
     # the engine picks up the new weights for the next self-play round
     trajs = MainSelfPlay(net, 2, S, seed=4).play()
     assert len(trajs) == 2
+
+
+def test_hip_forward_autograd_matches_torch():
+    """The unroll's HIP forward (k_initial_inference / k_recurrent_inference)
+    with torch backward: outputs and every parameter / input gradient equal
+    the all-torch graph's to fp32-conv tolerance."""
+    import mzgo
+    from mzgo.trainer import (initial_inference_hip, initial_inference_torch, recurrent_inference_hip,
+                              recurrent_inference_torch)
+    from oracle.positions import random_position
+    N, C, B = 5, 96, 7
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 2))
+    obs = torch.as_tensor(np.stack([random_position(N, 3 * b, b) for b in range(B)]), dtype=torch.float32).cuda()
+    act = torch.tensor([0, 3, A - 1, 7, 12, 1, 24]).cuda()
+    outs = {}
+    for name, f0, f in (("hip", initial_inference_hip, recurrent_inference_hip),
+                        ("torch", initial_inference_torch, recurrent_inference_torch)):
+        net.zero_grad()
+        lat, v0, lg0 = f0(net, obs)
+        x = lat
+        loss = (v0 ** 2).sum() + lg0.logsumexp(1).sum()
+        for k in range(3):
+            x, r, v, lg = f(net, x, act.roll(k))
+            loss = loss + (r ** 2).sum() + (v * 0.5).sum() + lg.logsumexp(1).sum() + 1e-3 * (x ** 2).sum()
+        loss.backward()
+        outs[name] = (loss.item(), {k: p.grad.detach().clone() for k, p in net.named_parameters()})
+    assert outs["hip"][0] == pytest.approx(outs["torch"][0], rel=1e-5)
+    for k, g in outs["torch"][1].items():
+        np.testing.assert_allclose(outs["hip"][1][k].cpu().numpy(), g.cpu().numpy(), rtol=1e-3,
+                                   atol=1e-5 * max(1.0, g.abs().max().item()), err_msg=k)
+
+
+def test_batched_step_hip_forward_equals_torch_forward():
+    import mzgo
+    from mzgo.trainer import MuZeroTrainer
+    from oracle.make_golden import synthetic_trajectories
+    N, C = 5, 96
+    A = N * N + 1
+    trajs = synthetic_trajectories(N, 6, seed=9)
+    res = {}
+    for hip in (True, False):
+        net = mzgo.MuZeroNet(C, A).cuda()
+        net.load_state_dict(mzgo.deterministic_state_dict(C, A, 4))
+        tr = MuZeroTrainer(net, mode="batched", start_index=lambda T: T // 3, hip_forward=hip)
+        res[hip] = (tr.train(_Buf(trajs), len(trajs)), dict(tr.last))
+    assert res[True][0] == pytest.approx(res[False][0], rel=1e-5)
+    for k in ("value_loss", "policy_loss", "reward_loss"):
+        assert res[True][1][k] == pytest.approx(res[False][1][k], rel=1e-5, abs=1e-7)
