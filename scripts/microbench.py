@@ -157,3 +157,54 @@ def move_stamps_report():
 
 if os.environ.get("MOVE_STAMPS"):
     move_stamps_report()
+
+
+def game_stamps_report():
+    """With MZGO_LIB=...libmzgo_stamps.so and GAME_STAMPS=1: phase cycles over
+    whole self-play games (every slot's stamps summed over all its moves),
+    mean over the G games, plus the slowest game's."""
+    import ctypes
+
+    import numpy as np
+    from mzgo import _lib
+    N = int(os.environ.get("N", 9))
+    G = int(os.environ.get("G", 256))
+    S = int(os.environ.get("S", 200))
+    C, A = 96, N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda().eval()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
+    sp = mzgo.SelfPlay(net, G, S)
+    fn = _lib.lib.mzgo_debug_stamps
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
+    buf = np.zeros((G, 91), np.uint64)
+    sp.reset()
+    sp.move(sp.max_moves)
+    torch.cuda.synchronize()
+    fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))      # drop the warm-up game
+    sp.reset(epoch=1)
+    c0 = sp.engine.counters()
+    ms = timeit(lambda: None, reps=1)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    sp.move(sp.max_moves)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b)
+    c1 = sp.engine.counters()
+    fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))
+    f = buf.astype(np.float64)
+    move_tot = f[:, 83:88].sum(1)
+    slow = int(np.argmax(move_tot))
+    names = ["board_load_record", "representation", "root_priors_dirichlet", "simulations", "choose_and_step"]
+    top = sorted([(int(i), float(f[:, i].mean())) for i in range(83) if f[:, i].mean() > 0], key=lambda x: -x[1])[:16]
+    print(json.dumps({"N": N, "G": G, "S": S, "game_ms": ms,
+                      "moves": c1["moves"] - c0["moves"], "convs": c1["dynamics_convs"] - c0["dynamics_convs"],
+                      "mean_game_cycles": float(move_tot.mean()), "max_game_cycles": float(move_tot.max()),
+                      "move_phases_mean": {n: round(float(f[:, 83 + k].mean())) for k, n in enumerate(names)},
+                      "move_phases_slowest": {n: round(float(f[slow, 83 + k])) for k, n in enumerate(names)},
+                      "search_slots_mean_top": [(i, round(v)) for i, v in top],
+                      "convs_slowest_game": float(f[slow, 59]), "convs_mean_game": float(f[:, 59].mean())}))
+
+
+if os.environ.get("GAME_STAMPS"):
+    game_stamps_report()
