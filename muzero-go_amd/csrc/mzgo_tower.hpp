@@ -62,10 +62,16 @@ struct TConvGeo {
   static constexpr int WSLOT = 3 * 64 * 64 * 2;         // one step's weight tile
   static constexpr int WPW = WSLOT / 1024 / NW;         // its 1-KiB pieces per wave
   static constexpr int MT = (G::TT + NW - 1) / NW;      // 16-pixel tiles per wave
+  // A-fragment prefetch distance in (tap, tile) groups (MZGO_TCONV_ADIST to experiment)
+#ifdef MZGO_TCONV_ADIST
+  static constexpr int ADIST = MZGO_TCONV_ADIST;
+#else
+  static constexpr int ADIST = 2;
+#endif
   static constexpr int LDS = 2 * PB + 2 * WSLOT + 4 * 64 * 4;
   static_assert(WPW * NW * 1024 == WSLOT, "whole weight pieces per wave");
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  static_assert(2 * PB >= G::CELLS * 272, "epilogue staging must fit the patch buffers");
+  static_assert(2 * PB >= G::CELLS * 272 + 9 * 64 * 4, "epilogue staging (+ E rows) must fit the patch buffers");
   // next chunk's patch pieces a wave issues at step ky (0, 1) of the current chunk
   __device__ static int pieces_at(int ky, int wave) {
     const int k0 = ky == 0 ? 0 : (NPW + 1) / 2, k1 = ky == 0 ? (NPW + 1) / 2 : NPW;
@@ -140,13 +146,20 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
 #ifdef MZGO_TCONV_STAMPS
 // diagnostic build: per-workgroup cycle sums (wave 0): 0 total, 1 prologue,
 // 2 vmcnt waits, 3 barriers, 4 MFMA steps, 5 epilogue, 6 launches
-__device__ unsigned long long g_tstamps[4096][8];
+__device__ unsigned long long g_tstamps[4096][8][8];   // [block][wave][field]
 #endif
 
 // 16 bytes of an MFMA fragment (one ds_read_b128).  (Two ds_read_b64 with
 // the halves of odd k-groups swapped on both operands are bank-conflict free
 // for 16 consecutive pixel rows, but measured 1.6x slower: b64 reads need
 // more waves per SIMD than this kernel has.)
+template <int K, typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int K, typename F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl<K>(f, std::make_integer_sequence<int, K>{}); }
+
 __device__ __forceinline__ bf16x8 frag_ld(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 #ifdef MZGO_TCONV_STAMPS
@@ -263,30 +276,47 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
         constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
         issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
       }
+      // One basic block per step (no per-tile branch: a wave past the last
+      // tile multiplies a clamped tile and drops it in the epilogue), as
+      // groups g = (tap kx, tile i): each group first issues the A fragments
+      // of group g + AD (and at i = 0 the B fragments of tap kx + 1), then
+      // runs its 8 MFMAs on fragments loaded AD groups (B: MT groups) ago.
+      constexpr int NG = 3 * T::MT, AD = T::ADIST;
       const char* ws = wring + (s & 1) * T::WSLOT;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
+      bf16x8 bf[2][4][2], af[AD + 1][2];
+      auto load_b = [&](int kx, bf16x8 (&d)[4][2]) {
         const char* wt = ws + kx * 64 * 64 * 2;
-        bf16x8 bf[4][2];
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-          bf[n][0] = frag_ld(wt + boff[n]);
-          bf[n][1] = frag_ld(wt + (boff[n] ^ 64));
+          d[n][0] = frag_ld(wt + boff[n]);
+          d[n][1] = frag_ld(wt + (boff[n] ^ 64));
         }
+      };
+      auto load_a = [&](auto gc) {
+        constexpr int g = decltype(gc)::value, kx = g / T::MT, i = g % T::MT;
+        const int q = qb[i] + ky * G::W + kx;
+        const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
+        af[g % (AD + 1)][0] = frag_ld(pbuf + off);
+        af[g % (AD + 1)][1] = frag_ld(pbuf + (off ^ 64));
+      };
+      load_b(0, bf[0]);
+      static_for<AD>([&](auto gc) { load_a(gc); });
+      auto group = [&](auto gc) {
+        constexpr int g = decltype(gc)::value, kx = g / T::MT, i = g % T::MT;
+        if constexpr (i == 0 && kx + 1 < 3) load_b(kx + 1, bf[(kx + 1) & 1]);
+        if constexpr (g + AD < NG) load_a(std::integral_constant<int, g + AD>{});
 #pragma unroll
-        for (int i = 0; i < T::MT; ++i) {
-          if (wave * T::MT + i >= G::TT) break;        // wave-uniform
-          const int q = qb[i] + ky * G::W + kx;
-          const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
-          const bf16x8 a0 = frag_ld(pbuf + off);
-          const bf16x8 a1 = frag_ld(pbuf + (off ^ 64));
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[n][0], acc[i][n], 0, 0, 0);
-            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[n][1], acc[i][n], 0, 0, 0);
-          }
+        for (int n = 0; n < 4; ++n) {
+          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g % (AD + 1)][0], bf[kx & 1][n][0], acc[i][n], 0, 0, 0);
+          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g % (AD + 1)][1], bf[kx & 1][n][1], acc[i][n], 0, 0, 0);
         }
-      }
+        // the group's reads first, then its 8 MFMAs, nothing moved across groups
+        constexpr int nrd = (i == 0 && kx + 1 < 3 ? 8 : 0) + (g + AD < NG ? 2 : 0);
+        if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for<NG>([&](auto gc) { group(gc); });
       STAMP_T(ts3);
 #ifdef MZGO_TCONV_STAMPS
       acc_wait += ts1 - ts0; acc_bar += ts2 - ts1; acc_mfma += ts3 - ts2;
@@ -299,7 +329,39 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
   lds_barrier();                                       // every wave's last reads done
   STAMP_T(tloop);
 
-  // epilogue 1: accumulators -> fp32 staging [cell][68] (over the patch buffers)
+  // epilogue: the residual pieces and the E[a] rows are fetched first (their
+  // latency overlaps the accumulator staging instead of every item waiting)
+  constexpr int NT = 64 * NW;
+  constexpr int ITEMS = (G::CELLS * 8 + NT - 1) / NT;   // (cell, 8-channel piece) items per thread
+  bf16* out = a.out + (long long)(a.out_idx ? a.out_idx[b] : b) * a.out_stride + (size_t)cg * G::P * 64;
+  const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
+                          : nullptr;
+  bf16x8 r8[ITEMS];
+  if (res) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = tid + k * NT;
+      if (idx < G::CELLS * 8) {
+        const int p = idx >> 3, y = p / N, x = p - y * N;
+        r8[k] = *reinterpret_cast<const bf16x8*>(res + tpix((y + 1) * G::W + (x + 1), idx & 7));
+      }
+    }
+  }
+  // E[a][region][this chunk's 64 couts] -> LDS behind the staging area
+  float* set = reinterpret_cast<float*>(lds) + G::CELLS * 68;
+  constexpr int EK = (9 * 64 + NT - 1) / NT;
+  float ev[EK];
+#pragma unroll
+  for (int k = 0; k < EK; ++k) ev[k] = 0.f;
+  if (a.etab) {
+    const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
+#pragma unroll
+    for (int k = 0; k < EK; ++k) {
+      const int i = tid + k * NT;
+      if (i < 9 * 64) ev[k] = eb[(size_t)(i >> 6) * CO * 64 + (i & 63)];
+    }
+  }
+  // accumulators -> fp32 staging [cell][68] (over the patch buffers)
   float* st = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < T::MT; ++i) {
@@ -313,13 +375,17 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
         if (p >= 0) st[p * 68 + n * 16 + (lane & 15)] = acc[i][n][r];
       }
   }
+  if (a.etab) {
+#pragma unroll
+    for (int k = 0; k < EK; ++k)
+      if (tid + k * NT < 9 * 64) set[tid + k * NT] = ev[k];
+  }
   __syncthreads();
-  // epilogue 2: 8 channels per thread: bias, E term, residual, ReLU, bf16 store, head partials
-  bf16* out = a.out + (long long)(a.out_idx ? a.out_idx[b] : b) * a.out_stride + (size_t)cg * G::P * 64;
-  const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
-                          : nullptr;
-  const float* et = a.etab ? a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64 : nullptr;
-  for (int idx = tid; idx < G::CELLS * 8; idx += 64 * NW) {
+  // 8 channels per thread and item: bias, E term, residual, ReLU, bf16 store, head partials
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int idx = tid + k * NT;
+    if (idx >= G::CELLS * 8) break;
     const int p = idx >> 3, j = idx & 7;
     const int y = p / N, x = p - y * N;
     const int q = (y + 1) * G::W + (x + 1);
@@ -327,35 +393,34 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
     const f32x4 s1 = *reinterpret_cast<const f32x4*>(st + p * 68 + j * 8 + 4);
     float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += sbias[j * 8 + k];
-    if (et) {
+    for (int e = 0; e < 8; ++e) v[e] += sbias[j * 8 + e];
+    if (a.etab) {
       const int reg = 3 * (y == 0 ? 0 : (y == N - 1 ? 2 : 1)) + (x == 0 ? 0 : (x == N - 1 ? 2 : 1));
-      const f32x4 e0 = *reinterpret_cast<const f32x4*>(et + (size_t)reg * CO * 64 + j * 8);
-      const f32x4 e1 = *reinterpret_cast<const f32x4*>(et + (size_t)reg * CO * 64 + j * 8 + 4);
+      const f32x4 e0 = *reinterpret_cast<const f32x4*>(set + reg * 64 + j * 8);
+      const f32x4 e1 = *reinterpret_cast<const f32x4*>(set + reg * 64 + j * 8 + 4);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { v[k] += e0[k]; v[k + 4] += e1[k]; }
+      for (int e = 0; e < 4; ++e) { v[e] += e0[e]; v[e + 4] += e1[e]; }
     }
     const int off = tpix(q, j);
     if (res) {
-      const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(res + off);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += (float)r8[k];
+      for (int e = 0; e < 8; ++e) v[e] += (float)r8[k][e];
     }
     bf16x8 o8;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o8[k] = (bf16)(v[k] > 0.f ? v[k] : 0.f);
+    for (int e = 0; e < 8; ++e) o8[e] = (bf16)(v[e] > 0.f ? v[e] : 0.f);
     *reinterpret_cast<bf16x8*>(out + off) = o8;
     if (a.headw) {
       float h[3];
 #pragma unroll
       for (int hh = 0; hh < 3; ++hh) {
-        float s = 0.f;
+        float sum = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += shw[hh * 64 + j * 8 + k] * (float)o8[k];
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        h[hh] = s;
+        for (int e = 0; e < 8; ++e) sum += shw[hh * 64 + j * 8 + e] * (float)o8[e];
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        sum += __shfl_xor(sum, 4);
+        h[hh] = sum;
       }
       if (j == 0) {
         float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
@@ -366,9 +431,9 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
     }
   }
 #ifdef MZGO_TCONV_STAMPS
-  if (tid == 0 && bid < 4096) {
+  if (lane == 0 && bid < 4096) {
     const unsigned long long tend = __builtin_amdgcn_s_memtime();
-    unsigned long long* g = g_tstamps[bid];
+    unsigned long long* g = g_tstamps[bid][wave];
     g[0] += tend - tstart; g[1] += tpro - tstart; g[2] += acc_wait; g[3] += acc_bar; g[4] += acc_mfma;
     g[5] += tend - tloop; g[6] += 1;
   }

@@ -26,7 +26,7 @@ hipError_t launch_tact(const int64_t* a, int* out, int B, int A, int* err, hipSt
 
 #ifdef MZGO_TCONV_STAMPS
 // Diagnostic builds only: k_tconv's per-workgroup cycle sums, summed over
-// workgroups (out[8]), then zeroed.
+// workgroups (out[64] = [wave][field]), then zeroed.
 extern "C" int mzgo_debug_tconv_stamps(unsigned long long* out) {
   // every instantiation has its own g_tstamps: read the 19x19 one
   return mzgo::tower_stamps_n19(out);

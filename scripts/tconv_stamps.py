@@ -14,7 +14,7 @@ sp = mzgo.SelfPlay(net, G, S, seed=1234)
 sp.reset()
 sp.move()
 torch.cuda.synchronize()
-out = (ctypes.c_ulonglong * 8)()
+out = (ctypes.c_ulonglong * 64)()
 f = _lib.lib.mzgo_debug_tconv_stamps
 f.argtypes = [ctypes.c_void_p]
 f(out)                       # zero after warmup
@@ -25,6 +25,7 @@ dt = time.perf_counter() - t0
 f(out)
 n = out[6]
 names = ["total", "prologue", "vmcnt waits", "barriers", "MFMA steps", "epilogue"]
-print(f"workgroup-launches {n}, move {dt*1e3:.1f} ms")
+print(f"workgroup-launches {n}, move {dt*1e3:.1f} ms  (wave 0; other waves per column)")
 for k, nm in enumerate(names):
-    print(f"  {nm:12s} {out[k] / max(n, 1):10.0f} cycles/launch  ({out[k] / max(out[0], 1) * 100:5.1f} %)")
+    per = " ".join(f"{out[w * 8 + k] / max(out[w * 8 + 6], 1):7.0f}" for w in range(8))
+    print(f"  {nm:12s} {out[k] / max(n, 1):10.0f} cycles/launch  ({out[k] / max(out[0], 1) * 100:5.1f} %)  waves: {per}")
