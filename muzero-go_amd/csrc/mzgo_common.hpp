@@ -78,8 +78,10 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // 32-43 per-wave conv-input work, 44-55 per-wave conv-input barrier wait,
 // 56-63 factored simulation detail (see sim_loop), 64-71 batch_expand detail,
 // 72-82 verify_batch / parent conv detail, 83-87 self-play move phases,
-// 88-90 representation convs
-constexpr int kStampPhases = 91;
+// 88-90 representation convs, 91-95 select counts (levels at depth >= 2,
+// selects, sequential-replay batches and their simulations, leaf depth sum)
+constexpr int kStampPhases = 96;
+constexpr int kStampLds = 91;          // phases >= this are thread 0's counters, kept in registers
 #ifdef MZGO_STAMPS
 // Phase sums accumulate in LDS (a global read-modify-write per lap would put
 // an HBM round trip on the measured wave's critical path); flush() adds them
@@ -89,9 +91,9 @@ struct Stamp {
   unsigned long long* lds;
   unsigned long long t;
   __device__ explicit Stamp(unsigned long long* b) : buf(b) {
-    __shared__ unsigned long long stamp_lds[kStampPhases];
+    __shared__ unsigned long long stamp_lds[kStampLds];
     lds = stamp_lds;
-    if (threadIdx.x < kStampPhases) lds[threadIdx.x] = 0;
+    if (threadIdx.x < kStampLds) lds[threadIdx.x] = 0;
     __syncthreads();
     t = __builtin_amdgcn_s_memtime();
   }
@@ -100,13 +102,20 @@ struct Stamp {
     if (threadIdx.x == 0) lds[phase] += now - t;
     t = now;
   }
+  unsigned long long xr[kStampPhases - kStampLds] = {};
   __device__ void wave_add(int phase, unsigned long long cycles) {
-    if ((threadIdx.x & 63) == 0) lds[phase] += cycles;   // one slot per wave
+    if (phase >= kStampLds) {
+      if (threadIdx.x == 0) xr[phase - kStampLds] += cycles;
+    } else if ((threadIdx.x & 63) == 0) {
+      lds[phase] += cycles;   // one slot per wave
+    }
   }
   __device__ unsigned long long now() const { return __builtin_amdgcn_s_memtime(); }
   __device__ void flush() {
     __syncthreads();
-    if (buf && threadIdx.x < kStampPhases) buf[blockIdx.x * kStampPhases + threadIdx.x] += lds[threadIdx.x];
+    if (buf && threadIdx.x < kStampLds) buf[blockIdx.x * kStampPhases + threadIdx.x] += lds[threadIdx.x];
+    if (buf && threadIdx.x == 0)
+      for (int k = 0; k < kStampPhases - kStampLds; ++k) buf[blockIdx.x * kStampPhases + kStampLds + k] += xr[k];
   }
 };
 #else

@@ -520,15 +520,21 @@ struct VerifyLds {
   int x[DMAX], n0[DMAX], N0[DMAX];
   double wpre[DMAX][G::A + 9];      // x_l's value sum after i accepted simulations (+ prefix_sums' tail)
   double wroot[G::A + 9];           // the root's value sum after i
-  uint64_t badm[DMAX][G::AP];       // simulations i whose x score is not finite at level l
   uint64_t failm[G::AP];            // simulations i whose walk leaves the batch (bit i)
   uint64_t exactm[DMAX][G::AP];     // (level, i) checks the screening left open
   int fail;
 };
-// leaf depths verify_batch handles (its arrays are per level; deeper paths
-// replay one select at a time): 8 at 9x9 and below, 2 at 19x19 (A = 362)
+// levels verify_batch holds at once (its arrays are per level; a deeper path
+// is checked in groups of this many levels): 8 at 9x9 and below, 2 at 19x19
 template <class G>
 constexpr int verify_depth() { return G::AP > 2 ? 2 : 8; }
+// leaves deeper than this replay their batch one select at a time instead
+// (MZGO_VERIFY_MAX_DEPTH to compare the two; the trees are the same)
+#ifdef MZGO_VERIFY_MAX_DEPTH
+constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
+#else
+constexpr int kVerifyMaxDepth = 1 << 20;
+#endif
 
 template <class G, class Acc>
 __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, Acc& T,
@@ -546,208 +552,214 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   const double* bv = sm.u.f.bv;
   // the node at depth d takes the share v (-1)^(D + 1 - d) of a batch child's backup
   if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
-  if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
-  // ---- 1a. jobs 0..D-1: level l's children (one wave each); jobs D..2D:
-  // the sequential value sums (the root's, then x_l's for each level) on
-  // other waves at the same time ----
-  for (int job = wave; job <= 2 * D; job += G::WAVES) {
-    if (job == D) {                                 // the root's value sum after i simulations
-      prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
-      continue;
-    }
-    if (job > D) {                                  // x_l = p_(l+1), depth l + 1
-      const int l = job - D - 1;
-      prefix_sums<G>(T.ws(T.path(l + 1)), bv, B, alt && ((D - l) & 1), vl.wpre[l]);
-      continue;
-    }
-    const int l = job;
-    const int p = T.path(l);
-    const int xa = l == 0 ? sm.t.ract : nact[T.path(l + 1)];
-    double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
-    int nx = 0;
+  // Levels l0 .. l0 + nl - 1 at a time (every (i, l) check is independent of
+  // the others; a failing i is recorded in failm whichever group finds it).
+  for (int l0 = 0; l0 < D; l0 += DV) {
+    const int nl = D - l0 < DV ? D - l0 : DV;
+    if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
+    // ---- 1a. jobs 0..nl-1: level l0 + k's children (one wave each); jobs
+    // nl..2nl-1: x's sequential value sums for those levels, and in the first
+    // group job 2nl: the root's, on other waves at the same time ----
+    const int njobs = 2 * nl + (l0 == 0 ? 1 : 0);
+    for (int job = wave; job < njobs; job += G::WAVES) {
+      if (job == 2 * nl) {                          // the root's value sum after i simulations
+        prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
+        continue;
+      }
+      if (job >= nl) {                              // x_l = p_(l+1), depth l + 1
+        const int k = job - nl, l = l0 + k;
+        prefix_sums<G>(T.ws(T.path(l + 1)), bv, B, alt && ((D - l) & 1), vl.wpre[k]);
+        continue;
+      }
+      const int k = job, l = l0 + k;
+      const int p = T.path(l);
+      const int xa = l == 0 ? sm.t.ract : nact[T.path(l + 1)];
+      double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
+      int nx = 0;
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      const bool in = a < G::A;
-      double P, w = 0.0;
-      int n = 0;
-      if (l == 0) {
-        P = in ? T.root_prior(a) : 0.0;
-        if constexpr (Acc::LDS) {
-          if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
+      for (int j = 0; j < G::AP; ++j) {
+        const int a = lane + 64 * j;
+        const bool in = a < G::A;
+        double P, w = 0.0;
+        int n = 0;
+        if (l == 0) {
+          P = in ? T.root_prior(a) : 0.0;
+          if constexpr (Acc::LDS) {
+            if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
+          } else {
+            const int c = in ? T.child(0, a) : -1;
+            if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+          }
         } else {
-          const int c = in ? T.child(0, a) : -1;
+          P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
+          const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
           if (c >= 0) { n = T.vis(c); w = T.ws(c); }
         }
-      } else {
-        P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
-        const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
-        if (c >= 0) { n = T.vis(c); w = T.ws(c); }
-      }
-      const bool e = P > 0.0;
-      const uint64_t el = __ballot(e);
-      const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
-      const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
-      vl.cP[l][a] = cp;
-      vl.q[l][a] = q;
-      vl.inv1n[l][a] = 1.0 / (double)(1 + n);
-      vl.n[l][a] = n;
-      if (lane == 0) vl.elig[l][j] = el;
-      if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
-      if (j == (xa >> 6)) {
-        nx = __builtin_amdgcn_readlane(n, xa & 63);
-        cpx = dpp::lane(cp, xa & 63);
-      }
-    }
-    wave_minmax(lo, hi);
-    if (lane == 0) {
-      vl.lo_o[l] = lo;
-      vl.hi_o[l] = hi;
-      vl.x[l] = xa;
-      vl.n0[l] = nx;
-      vl.N0[l] = T.vis(p);
-      vl.cpx[l] = cpx;
-    }
-    if (st) st->lap(75);
-  }
-  __syncthreads();
-  if (st) st->lap(76);
-  // ---- 1b. per level, per simulation i (lane i = lane + 64 j): the level
-  // as simulation i's select finds it, and x's score exactly as puct_pick
-  // forms it ----
-  for (int l = wave; l < D; l += G::WAVES) {
-    const int nx = vl.n0[l], N0 = vl.N0[l];
-    const double lo = vl.lo_o[l], hi = vl.hi_o[l], cpx = vl.cpx[l];
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const int i = lane + 64 * j;
-      bool bad = false;
-      if (i <= B) {
-        const int n1 = nx + i, Ni = N0 + i;
-        const double qxi = n1 > 0 ? vl.wpre[l][i] / (double)n1 : 0.0;
-        const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
-        const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
-        const double sxi = (hii > loi ? (qxi - loi) / (hii - loi) : qxi) + (cpx * sqi) / (double)(1 + n1);
-        vl.qx[l][i] = qxi;
-        vl.invr[l][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;
-        vl.sq[l][i] = sqi;
-        vl.sx[l][i] = sxi;
-        bad = i >= 1 && i < B && !(sxi > -INFINITY);
-      }
-      const uint64_t bb = __ballot(bad);
-      if (lane == 0) vl.badm[l][j] = bb;
-    }
-    if (st) st->lap(77);
-  }
-  __syncthreads();
-  if (st) st->lap(72);
-  // ---- 2. every (i, l) check at once, transposed: lanes are simulations
-  // i = lane + 64 j, each wave takes every WAVES-th child a of each level.
-  // Screening: the two divisions of a's score as products with reciprocals
-  // (a few ulp off); a decides (l, i) only if its score is clear of x's by
-  // far more than that, else (l, i) is redone below with puct_pick's exact
-  // operations.  i fails if any eligible a != x beats x (puct_pick's first
-  // maximum: a higher score, or an equal one at a lower action). ----
-  const unsigned long long ts0 = st ? st->now() : 0;
-  for (int l = 0; l < D; ++l) {
-    const int xa = vl.x[l];
-    const double lo_o = vl.lo_o[l], hi_o = vl.hi_o[l];
-    double loi[G::AP], invr[G::AP], sqi[G::AP], sxi[G::AP], tol[G::AP];
-    bool spread[G::AP];
-    uint64_t beaten[G::AP], close[G::AP];
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const int i = lane + 64 * j;
-      const int ii = i <= B ? i : B;
-      const double qxi = vl.qx[l][ii];
-      loi[j] = fmin(lo_o, qxi);
-      spread[j] = fmax(hi_o, qxi) > loi[j];
-      invr[j] = vl.invr[l][ii];
-      sqi[j] = vl.sq[l][ii];
-      sxi[j] = vl.sx[l][ii];
-      tol[j] = 1e-12 * (1.0 + fabs(sxi[j]));
-      beaten[j] = 0;
-      close[j] = 0;
-    }
-    // the wave's children a = wave + WAVES k, one per lane k, loaded in one
-    // round trip; the loop broadcasts them with readlane
-    constexpr int KW = (G::A + G::WAVES - 1) / G::WAVES;
-    static_assert(KW <= 64, "one lane per child of the wave");
-    const int amine = wave + G::WAVES * lane;
-    const bool mine = lane < KW && amine < G::A && amine != xa &&
-                      ((vl.elig[l][(amine < G::A ? amine : 0) >> 6] >> (amine & 63)) & 1ull);
-    const int ac = mine ? amine : 0;
-    const double qa_l = vl.q[l][ac], cpa_l = vl.cP[l][ac], ia_l = vl.inv1n[l][ac];
-    const uint64_t todo = __ballot(mine);
-    for (uint64_t mm = todo; mm; mm &= mm - 1) {
-      const int k = __builtin_ctzll(mm);
-      const double qa = dpp::lane(qa_l, k), cpa = dpp::lane(cpa_l, k), ia = dpp::lane(ia_l, k);
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        if (64 * j >= B) break;                     // (uniform) no simulation i in this register
-        const double sc = (spread[j] ? (qa - loi[j]) * invr[j] : qa) + (cpa * sqi[j]) * ia;
-        beaten[j] |= __ballot(sc > sxi[j] + tol[j]);
-        close[j] |= __ballot(!(fabs(sc - sxi[j]) > tol[j]));
-      }
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        if (beaten[j]) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)beaten[j]);
-        if (close[j] & ~beaten[j])
-          atomicOr(reinterpret_cast<unsigned long long*>(&vl.exactm[l][j]), (unsigned long long)(close[j] & ~beaten[j]));
-      }
-    }
-  }
-  if (st) st->wave_add(80, st->now() - ts0);
-  __syncthreads();
-  if (st) st->lap(78);
-  // the open (l, i) checks with puct_pick's exact operations (rare)
-  for (int l = 0; l < D; ++l) {
-    uint64_t open[G::AP];
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const uint64_t o = vl.exactm[l][j] & ~vl.failm[j];
-      open[j] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
-                __builtin_amdgcn_readfirstlane((uint32_t)o);
-    }
-    int k = 0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      for (uint64_t mm = open[j]; mm; mm &= mm - 1, ++k) {
-        if (k % G::WAVES != wave) continue;
-        const int i = 64 * j + __builtin_ctzll(mm);
-        if (i < 1 || i >= B) continue;
-        const int xa = vl.x[l];
-        const int nx = vl.n0[l] + i;
-        const double qx = vl.qx[l][i];
-        const double lo = fmin(vl.lo_o[l], qx), hi = fmax(vl.hi_o[l], qx);
-        const double sq = vl.sq[l][i], sx = vl.sx[l][i];
-        uint64_t beat = 0;
-#pragma unroll
-        for (int jj = 0; jj < G::AP; ++jj) {
-          const int a = lane + 64 * jj;
-          const bool el = (vl.elig[l][jj] >> lane) & 1ull;
-          const bool isx = a == xa;
-          const double q = isx ? qx : vl.q[l][a];
-          const int n = isx ? nx : vl.n[l][a];
-          const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
-          const double sc = qn + (vl.cP[l][a] * sq) / (double)(1 + n);
-          beat |= __ballot(el && !isx && (sc > sx || (sc == sx && a < xa)));
+        const bool e = P > 0.0;
+        const uint64_t el = __ballot(e);
+        const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
+        const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
+        vl.cP[k][a] = cp;
+        vl.q[k][a] = q;
+        vl.inv1n[k][a] = 1.0 / (double)(1 + n);
+        vl.n[k][a] = n;
+        if (lane == 0) vl.elig[k][j] = el;
+        if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
+        if (j == (xa >> 6)) {
+          nx = __builtin_amdgcn_readlane(n, xa & 63);
+          cpx = dpp::lane(cp, xa & 63);
         }
-        if (beat && lane == 0)
-          atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[i >> 6]), 1ull << (i & 63));
+      }
+      wave_minmax(lo, hi);
+      if (lane == 0) {
+        vl.lo_o[k] = lo;
+        vl.hi_o[k] = hi;
+        vl.x[k] = xa;
+        vl.n0[k] = nx;
+        vl.N0[k] = T.vis(p);
+        vl.cpx[k] = cpx;
+      }
+      if (st) st->lap(75);
+    }
+    __syncthreads();
+    if (st) st->lap(76);
+    // ---- 1b. per level, per simulation i (lane i = lane + 64 j): the level
+    // as simulation i's select finds it, and x's score exactly as puct_pick
+    // forms it; a score that is not finite fails i ----
+    for (int k = wave; k < nl; k += G::WAVES) {
+      const int nx = vl.n0[k], N0 = vl.N0[k];
+      const double lo = vl.lo_o[k], hi = vl.hi_o[k], cpx = vl.cpx[k];
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int i = lane + 64 * j;
+        bool bad = false;
+        if (i <= B) {
+          const int n1 = nx + i, Ni = N0 + i;
+          const double qxi = n1 > 0 ? vl.wpre[k][i] / (double)n1 : 0.0;
+          const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
+          const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
+          const double sxi = (hii > loi ? (qxi - loi) / (hii - loi) : qxi) + (cpx * sqi) / (double)(1 + n1);
+          vl.qx[k][i] = qxi;
+          vl.invr[k][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;
+          vl.sq[k][i] = sqi;
+          vl.sx[k][i] = sxi;
+          bad = i >= 1 && i < B && !(sxi > -INFINITY);
+        }
+        const uint64_t bb = __ballot(bad);
+        if (lane == 0 && bb) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)bb);
+      }
+      if (st) st->lap(77);
+    }
+    __syncthreads();
+    if (st) st->lap(72);
+    // ---- 2. every (i, l) check at once, transposed: lanes are simulations
+    // i = lane + 64 j, each wave takes every WAVES-th child a of each level.
+    // Screening: the two divisions of a's score as products with reciprocals
+    // (a few ulp off); a decides (l, i) only if its score is clear of x's by
+    // far more than that, else (l, i) is redone below with puct_pick's exact
+    // operations.  i fails if any eligible a != x beats x (puct_pick's first
+    // maximum: a higher score, or an equal one at a lower action). ----
+    const unsigned long long ts0 = st ? st->now() : 0;
+    for (int k = 0; k < nl; ++k) {
+      const int xa = vl.x[k];
+      const double lo_o = vl.lo_o[k], hi_o = vl.hi_o[k];
+      double loi[G::AP], invr[G::AP], sqi[G::AP], sxi[G::AP], tol[G::AP];
+      bool spread[G::AP];
+      uint64_t beaten[G::AP], close[G::AP];
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const int i = lane + 64 * j;
+        const int ii = i <= B ? i : B;
+        const double qxi = vl.qx[k][ii];
+        loi[j] = fmin(lo_o, qxi);
+        spread[j] = fmax(hi_o, qxi) > loi[j];
+        invr[j] = vl.invr[k][ii];
+        sqi[j] = vl.sq[k][ii];
+        sxi[j] = vl.sx[k][ii];
+        tol[j] = 1e-12 * (1.0 + fabs(sxi[j]));
+        beaten[j] = 0;
+        close[j] = 0;
+      }
+      // the wave's children a = wave + WAVES k, one per lane k, loaded in one
+      // round trip; the loop broadcasts them with readlane
+      constexpr int KW = (G::A + G::WAVES - 1) / G::WAVES;
+      static_assert(KW <= 64, "one lane per child of the wave");
+      const int amine = wave + G::WAVES * lane;
+      const bool mine = lane < KW && amine < G::A && amine != xa &&
+                        ((vl.elig[k][(amine < G::A ? amine : 0) >> 6] >> (amine & 63)) & 1ull);
+      const int ac = mine ? amine : 0;
+      const double qa_l = vl.q[k][ac], cpa_l = vl.cP[k][ac], ia_l = vl.inv1n[k][ac];
+      const uint64_t todo = __ballot(mine);
+      for (uint64_t mm = todo; mm; mm &= mm - 1) {
+        const int kk = __builtin_ctzll(mm);
+        const double qa = dpp::lane(qa_l, kk), cpa = dpp::lane(cpa_l, kk), ia = dpp::lane(ia_l, kk);
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j) {
+          if (64 * j >= B) break;                     // (uniform) no simulation i in this register
+          const double sc = (spread[j] ? (qa - loi[j]) * invr[j] : qa) + (cpa * sqi[j]) * ia;
+          beaten[j] |= __ballot(sc > sxi[j] + tol[j]);
+          close[j] |= __ballot(!(fabs(sc - sxi[j]) > tol[j]));
+        }
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j) {
+          if (beaten[j]) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)beaten[j]);
+          if (close[j] & ~beaten[j])
+            atomicOr(reinterpret_cast<unsigned long long*>(&vl.exactm[k][j]), (unsigned long long)(close[j] & ~beaten[j]));
+        }
       }
     }
+    if (st) st->wave_add(80, st->now() - ts0);
+    __syncthreads();
+    if (st) st->lap(78);
+    // the open (l, i) checks with puct_pick's exact operations (rare)
+    for (int k = 0; k < nl; ++k) {
+      uint64_t open[G::AP];
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        const uint64_t o = vl.exactm[k][j] & ~vl.failm[j];
+        open[j] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+                  __builtin_amdgcn_readfirstlane((uint32_t)o);
+      }
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        for (uint64_t mm = open[j]; mm; mm &= mm - 1, ++c) {
+          if (c % G::WAVES != wave) continue;
+          const int i = 64 * j + __builtin_ctzll(mm);
+          if (i < 1 || i >= B) continue;
+          const int xa = vl.x[k];
+          const int nx = vl.n0[k] + i;
+          const double qx = vl.qx[k][i];
+          const double lo = fmin(vl.lo_o[k], qx), hi = fmax(vl.hi_o[k], qx);
+          const double sq = vl.sq[k][i], sx = vl.sx[k][i];
+          uint64_t beat = 0;
+#pragma unroll
+          for (int jj = 0; jj < G::AP; ++jj) {
+            const int a = lane + 64 * jj;
+            const bool el = (vl.elig[k][jj] >> lane) & 1ull;
+            const bool isx = a == xa;
+            const double q = isx ? qx : vl.q[k][a];
+            const int n = isx ? nx : vl.n[k][a];
+            const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
+            const double sc = qn + (vl.cP[k][a] * sq) / (double)(1 + n);
+            beat |= __ballot(el && !isx && (sc > sx || (sc == sx && a < xa)));
+          }
+          if (beat && lane == 0)
+            atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[i >> 6]), 1ull << (i & 63));
+        }
+      }
+    }
+    __syncthreads();
+    if (st) st->lap(79);
   }
-  __syncthreads();
-  if (st) st->lap(79);
+  if (D == 0 && threadIdx.x == 0) prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
   if (threadIdx.x == 0) {
     int f = B;
 #pragma unroll
     for (int j = G::AP - 1; j >= 0; --j) {
       uint64_t mm = vl.failm[j];
-      for (int l = 0; l < D; ++l) mm |= vl.badm[l][j];
       if (j == 0) mm &= ~1ull;                         // (simulation i = 0 reached the leaf already)
       if (mm) f = 64 * j + __builtin_ctzll(mm);
     }
@@ -756,16 +768,23 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   __syncthreads();
   if (st) st->lap(73);
   const int m = vl.fail;
-  // ---- 3. the tree takes the m accepted simulations ----
+  // ---- 3. the tree takes the m accepted simulations: path node p_d (d >= 1)
+  // gets m visits and the first m of its shares, summed in simulation order
+  // (prefix_sums' f64 chain, one lane per node) ----
   if (wave_id() == 0) {
-    if (lane <= D) {                                // path nodes p_0 .. p_D
-      if (lane == 0) {
+    for (int d = lane; d <= D; d += 64) {
+      if (d == 0) {
         T.set(0, T.vis(0) + m, vl.wroot[m]);
       } else {
-        const int l = lane - 1;                     // p_lane = x_l
-        T.set(T.path(lane), vl.n0[l] + m, vl.wpre[l][m]);
+        const int p = T.path(d);
+        const bool neg = alt && ((D + 1 - d) & 1);
+        double w = T.ws(p);
+#pragma unroll 8
+        for (int k = 0; k < m; ++k) w = w + (neg ? -bv[k] : bv[k]);
+        const int n = T.vis(p) + m;
+        T.set(p, n, w);
         if constexpr (Acc::LDS)
-          if (lane == 1) { sm.t.rvis[sm.t.ract] = vl.n0[0] + m; sm.t.rws[sm.t.ract] = vl.wpre[0][m]; }
+          if (d == 1) { sm.t.rvis[sm.t.ract] = n; sm.t.rws[sm.t.ract] = w; }
       }
     }
     wave_lds_sync();
@@ -830,6 +849,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       if (wave_id() == 0) {
         const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st);
         if (lane_id() == 0) sm.t.action = a;
+        st.wave_add(92, 1);
+        st.wave_add(95, (unsigned long long)sm.t.depth);
       }
       __syncthreads();
     }
@@ -896,7 +917,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
         __syncthreads();
         st.lap(5);
-        if (depth <= verify_depth<G>()) {
+        if (depth <= kVerifyMaxDepth) {
           const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
           nodes += m;
           sim += m;
@@ -915,6 +936,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
               const int ai = sm.u.f.acts[i];
               if (i > 0) {
                 const int a2 = select_leaf<G>(sm.t, T, sp, key, sim + i, &st);
+                st.wave_add(92, 1);
+                st.wave_add(95, (unsigned long long)sm.t.depth);
                 if (a2 != ai || sm.t.leaf != leaf) {           // prediction ends: a2 is sim + i's select
                   if (lane == 0) sm.t.action = a2;
                   break;
@@ -931,6 +954,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
             }
           }
           if (lane == 0) sm.t.bcast = m;
+          st.wave_add(93, 1);
+          st.wave_add(94, (unsigned long long)m);
         }
         __syncthreads();
         const int m = sm.t.bcast;
@@ -1354,7 +1379,11 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   // pp.moves moves of this game in one launch (the board stays in LDS between
   // them): a game's moves run back to back on its CU instead of every move of
   // every game waiting for the slowest game's move at a launch boundary
+#ifdef MZGO_ONE_MOVE
+  for (int step = 0; step < 1; ++step) {             // (experiment: the loop's register cost)
+#else
   for (int step = 0; step < pp.moves; ++step) {
+#endif
 #ifdef MZGO_STAMPS
   unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   tm[0] = __builtin_amdgcn_s_memtime();

@@ -821,7 +821,10 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     depth += 1;
     if (lane == 0) const_cast<Acc&>(T).set_path(depth, best_c);
     node = best_c;
-    if (st) st->lap(depth == 1 ? 22 : 23);
+    if (st) {
+      st->lap(depth == 1 ? 22 : 23);
+      if (depth >= 2) st->wave_add(91, 1);
+    }
   }
   t.leaf = node;
   t.depth = depth;

@@ -73,7 +73,7 @@ def stamps_report():
     obs = torch.zeros(G, 6, N, N)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 91), np.uint64)
+    buf = np.zeros((G, 96), np.uint64)
     seng.search(obs)
     torch.cuda.synchronize()
     fn(seng.handle, buf.ctypes.data_as(ctypes.c_void_p))          # drop the warm-up
@@ -139,7 +139,7 @@ def move_stamps_report():
     sp.reset()
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 91), np.uint64)
+    buf = np.zeros((G, 96), np.uint64)
     sp.move()
     torch.cuda.synchronize()
     fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))
@@ -176,7 +176,7 @@ def game_stamps_report():
     sp = mzgo.SelfPlay(net, G, S)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 91), np.uint64)
+    buf = np.zeros((G, 96), np.uint64)
     sp.reset()
     sp.move(sp.max_moves)
     torch.cuda.synchronize()
@@ -203,7 +203,15 @@ def game_stamps_report():
                       "move_phases_mean": {n: round(float(f[:, 83 + k].mean())) for k, n in enumerate(names)},
                       "move_phases_slowest": {n: round(float(f[slow, 83 + k])) for k, n in enumerate(names)},
                       "search_slots_mean_top": [(i, round(v)) for i, v in top],
-                      "convs_slowest_game": float(f[slow, 59]), "convs_mean_game": float(f[:, 59].mean())}))
+                      "convs_slowest_game": float(f[slow, 59]), "convs_mean_game": float(f[:, 59].mean()),
+                      "wall_slots_mean": {i: round(float(f[:, i].mean())) for i in
+                                          (0, 2, 3, 4, 5, 22, 23, 24, 25, 26, 27, 62, 63, 69, 70, 71, 72, 73, 74,
+                                           75, 76, 77, 78, 79, 81, 82)},
+                      "selects_per_game": float(f[:, 92].mean()), "deep_levels_per_game": float(f[:, 91].mean()),
+                      "mean_leaf_depth": float(f[:, 95].sum() / max(f[:, 92].sum(), 1)),
+                      "batches_per_game": float(f[:, 31].mean()), "batched_sims_per_game": float(f[:, 28].mean()),
+                      "seq_replay_batches_per_game": float(f[:, 93].mean()),
+                      "seq_replay_sims_per_game": float(f[:, 94].mean())}))
 
 
 if os.environ.get("GAME_STAMPS"):
