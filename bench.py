@@ -422,7 +422,7 @@ def main():
                       convs=(c1["dynamics_convs"] - c0["dynamics_convs"]))
         roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload, args.moves_per_launch)
         out = {
-            "metric": "MCTS simulations/sec (whole node) + self-play moves/sec, 9x9 Go, 200 sims/move",
+            "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {S} sims/move",
             "value": sims / dt,
             "unit": "sims/s",
             "n_gpus": world,

@@ -446,20 +446,20 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     if (threadIdx.x == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
     __syncthreads();
     if (st) st->lap(61);
+    // the simulations' choices: sim k takes the r_k-th (ascending) of the
+    // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
+    uint64_t el[G::AP];
+    int n = 0;
     if (wave_id() == 0) {
-      // the simulations' choices: sim k takes the r_k-th (ascending) of the
-      // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
       const int lane = lane_id_local();
-      uint64_t el[G::AP];
-      int n = 0;
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) {
         const int a = lane + 64 * j;
         el[j] = __ballot(a < G::A && T.root_prior(a) > 0.0);
         n += __popcll(el[j]);
       }
-      pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
     }
+    if (wave_id() == 0) pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
     batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, pool, st);
     __syncthreads();
     if (st) st->lap(62);
@@ -904,13 +904,13 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         if (threadIdx.x == 0) { sm.u.f.acts[0] = a; sm.t.npick = 1; sm.t.ngrab = 0; }
         __syncthreads();
         st.lap(70);
+        uint64_t um[G::AP];
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j) um[j] = sm.t.umask[j];
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j)
+          if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
         if (wave_id() == 0) {
-          uint64_t um[G::AP];
-#pragma unroll
-          for (int j = 0; j < G::AP; ++j) um[j] = sm.t.umask[j];
-#pragma unroll
-          for (int j = 0; j < G::AP; ++j)
-            if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
           pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1);
           st.lap(71);
         }

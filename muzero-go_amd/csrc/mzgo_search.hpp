@@ -569,24 +569,24 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 // one.  out[i0 + i] (LDS) gets the actions; *progress (LDS, if given) is
 // published after the first `head` picks and every 12 after.  Wave-level.
 template <class G>
-__device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
-                                              int sim0, int* out, int* progress = nullptr, int head = 1) {
-  const int lane = lane_id_local();
-  uint32_t r[G::AP];
+struct PickSeq {
+  uint32_t r[G::AP];       // lane i = lane + 64 q: simulation i's rank among the remaining
+  uint64_t rem[G::AP];     // the remaining elements (wave-uniform)
+  uint32_t rank[G::AP];    // lane a = lane + 64 j: element a's rank among them
+  __device__ __forceinline__ PickSeq() {}
+  __device__ __forceinline__ PickSeq(const uint64_t (&m)[G::AP], int n, int count, uint64_t key, int sim0) {
+    const int lane = lane_id_local();
 #pragma unroll
-  for (int q = 0; q < G::AP; ++q) {
-    const int i = lane + 64 * q;
-    r[q] = i < count ? randbelow(draw(key, TAG_SELECT, (uint64_t)(sim0 + i)), (uint32_t)(n - i)) : 0u;
-  }
-  uint64_t rem[G::AP];
+    for (int q = 0; q < G::AP; ++q) {
+      const int i = lane + 64 * q;
+      r[q] = i < count ? randbelow(draw(key, TAG_SELECT, (uint64_t)(sim0 + i)), (uint32_t)(n - i)) : 0u;
+    }
 #pragma unroll
-  for (int j = 0; j < G::AP; ++j) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m[j]);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m[j] >> 32));
-    rem[j] = ((uint64_t)hi << 32) | lo;
-  }
-  uint32_t rank[G::AP];
-  {
+    for (int j = 0; j < G::AP; ++j) {
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m[j]);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m[j] >> 32));
+      rem[j] = ((uint64_t)hi << 32) | lo;
+    }
     uint32_t below = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
@@ -595,8 +595,9 @@ __device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n,
       below += (uint32_t)__popcll(rem[j]);
     }
   }
-  int next_pub = head < count ? head : count;
-  for (int i = 0; i < count; ++i) {
+  // pick i (in order i = 0, 1, ...): the remaining element of rank r_i
+  __device__ __forceinline__ int pick(int i) {
+    const int lane = lane_id_local();
     uint32_t ri = 0;
 #pragma unroll
     for (int q = 0; q < G::AP; ++q)
@@ -613,6 +614,18 @@ __device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n,
       if ((a >> 6) == j) rem[j] &= ~(1ull << (a & 63));
       rank[j] -= (lane + 64 * j > a) ? 1u : 0u;
     }
+    return a;
+  }
+};
+
+template <class G>
+__device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
+                                              int sim0, int* out, int* progress = nullptr, int head = 1) {
+  const int lane = lane_id_local();
+  PickSeq<G> ps(m, n, count, key, sim0);
+  int next_pub = head < count ? head : count;
+  for (int i = 0; i < count; ++i) {
+    const int a = ps.pick(i);
     if (lane == 0) out[i0 + i] = a;
     if (progress && i + 1 == next_pub) {
       wave_lds_sync();

@@ -125,24 +125,6 @@ struct TConvArgs {
 template <class G, int T>
 struct TapOff { static constexpr int v = (T / 3) * G::W + (T % 3); };
 
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63]
-__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
-  switch (n) {
-#define MZGO_W(k) case k: wait_vmcnt<k>(); break;
-    MZGO_W(0) MZGO_W(1) MZGO_W(2) MZGO_W(3) MZGO_W(4) MZGO_W(5) MZGO_W(6) MZGO_W(7) MZGO_W(8) MZGO_W(9)
-    MZGO_W(10) MZGO_W(11) MZGO_W(12) MZGO_W(13) MZGO_W(14) MZGO_W(15) MZGO_W(16) MZGO_W(17) MZGO_W(18)
-    MZGO_W(19) MZGO_W(20) MZGO_W(21) MZGO_W(22) MZGO_W(23) MZGO_W(24) MZGO_W(25) MZGO_W(26) MZGO_W(27)
-    MZGO_W(28) MZGO_W(29) MZGO_W(30) MZGO_W(31)
-#undef MZGO_W
-    default: wait_vmcnt<0>(); break;
-  }
-}
-
 #ifdef MZGO_TCONV_STAMPS
 // diagnostic build: per-workgroup cycle sums (wave 0): 0 total, 1 prologue,
 // 2 vmcnt waits, 3 barriers, 4 MFMA steps, 5 epilogue, 6 launches

@@ -211,7 +211,8 @@ def game_stamps_report():
                       "mean_leaf_depth": float(f[:, 95].sum() / max(f[:, 92].sum(), 1)),
                       "batches_per_game": float(f[:, 31].mean()), "batched_sims_per_game": float(f[:, 28].mean()),
                       "seq_replay_batches_per_game": float(f[:, 93].mean()),
-                      "seq_replay_sims_per_game": float(f[:, 94].mean())}))
+                      "seq_replay_sims_per_game": float(f[:, 94].mean()),
+                      "expand_slots_64_68_total": [round(float(f[:, i].mean())) for i in (64, 65, 66, 67, 68)]}))
 
 
 if os.environ.get("GAME_STAMPS"):
