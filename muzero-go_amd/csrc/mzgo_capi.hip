@@ -188,7 +188,6 @@ struct mzgo_engine {
   float* d_w = nullptr;
   size_t d_w_bytes = 0;
   NetParams np{};
-  NetParams* d_np = nullptr;   // device copy of np (k_selfplay_move reads it through a pointer)
   EngineArrays E{};
   int* d_err = nullptr;
   float* d_scr = nullptr;      // initial_inference scratch (strip boards), grown on demand
@@ -284,7 +283,6 @@ struct mzgo_engine {
     np.hs.fc2_w = b + off[14]; np.hs.fc2_b = b + off[15]; np.hs.value_b = b + off[16];
     np.hs.vfc_w = b + off[17]; np.hs.vfc_b = b + off[18]; np.hs.policy_b = b + off[19];
     np.hs.pass_logit = b + off[20];
-    HIPCHK(hipMemcpy(d_np, &np, sizeof np, hipMemcpyHostToDevice));
     dirty = false;
     return MZGO_OK;
   }
@@ -435,7 +433,6 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     }
   }
   if (C != 0) {
-    chk(e->alloc(&e->d_np, 1));
     chk(e->alloc(&E.prior, G * n1 * A));
     chk(e->alloc(&E.child, G * n1 * A));
     chk(e->alloc(&E.visits, G * n1));
@@ -680,7 +677,7 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
     }
     return MZGO_OK;
   }
-  HIPCHK(e->ks->selfplay_move(e->d_np, e->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  HIPCHK(e->ks->selfplay_move(e->np, e->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
 
@@ -707,7 +704,7 @@ int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* str
   pp.noise = e->noise;
   pp.arena = 1;
   pp.moves = moves;
-  HIPCHK(e->ks->selfplay_move(e->d_np, opponent->d_np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
+  HIPCHK(e->ks->selfplay_move(e->np, opponent->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
   return MZGO_OK;
 }
 

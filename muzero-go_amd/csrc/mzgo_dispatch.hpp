@@ -21,7 +21,7 @@ struct KernelSet {
   hipError_t (*board_step)(const EngineArrays&, int G, const int* act, int* status, double* winner,
                            double komi, hipStream_t);
   hipError_t (*board_planes)(const EngineArrays&, int G, double* planes, hipStream_t);
-  hipError_t (*selfplay_move)(const NetParams* np_dev, const NetParams* np_b_dev, const SearchParams&,
+  hipError_t (*selfplay_move)(const NetParams& np, const NetParams& np_b, const SearchParams&,
                               const PlayParams&, const EngineArrays&, int G, hipStream_t);
 };
 
@@ -61,7 +61,7 @@ struct Launch {
     hipLaunchKernelGGL((k_board_planes<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, E, planes);
     return hipGetLastError();
   }
-  static hipError_t move(const NetParams* np, const NetParams* np_b, const SearchParams& sp,
+  static hipError_t move(const NetParams& np, const NetParams& np_b, const SearchParams& sp,
                          const PlayParams& pp, const EngineArrays& E, int G, hipStream_t s) {
     hipLaunchKernelGGL((k_selfplay_move<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, np, np_b, sp, pp, E);
     return hipGetLastError();

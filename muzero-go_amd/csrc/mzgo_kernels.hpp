@@ -24,6 +24,19 @@ struct NetParams {
   HeadScalars hs;
 };
 
+// b ? x : y, field by field (kernel-argument pointers stay known-global, so
+// their loads are global loads, not flat ones)
+__device__ __forceinline__ NetParams select_params(bool b, const NetParams& x, const NetParams& y) {
+  NetParams n;
+#define MZGO_SEL(f) n.f = b ? x.f : y.f;
+  MZGO_SEL(w_conv1) MZGO_SEL(b_conv1) MZGO_SEL(w_conv2) MZGO_SEL(b_conv2) MZGO_SEL(w_conv3) MZGO_SEL(b_conv3)
+  MZGO_SEL(w_dyn) MZGO_SEL(b_dyn) MZGO_SEL(emb) MZGO_SEL(head_w) MZGO_SEL(etab)
+  MZGO_SEL(hs.reward_b) MZGO_SEL(hs.fc1_w) MZGO_SEL(hs.fc1_b) MZGO_SEL(hs.fc2_w) MZGO_SEL(hs.fc2_b)
+  MZGO_SEL(hs.value_b) MZGO_SEL(hs.vfc_w) MZGO_SEL(hs.vfc_b) MZGO_SEL(hs.policy_b) MZGO_SEL(hs.pass_logit)
+#undef MZGO_SEL
+  return n;
+}
+
 // Per-slot device state of an engine (sizes fixed at engine creation).
 struct EngineArrays {
   int S;                 // simulations per move this engine was sized for
@@ -1367,7 +1380,7 @@ struct PlayParams {
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(const NetParams* __restrict__ np_a, const NetParams* __restrict__ np_b,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np_a, NetParams np_b,
                                                              SearchParams sp, PlayParams pp, EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
@@ -1393,9 +1406,9 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const int mv = m.moves;
   // arena (main.py:535-549): turn 0 = "current" (np_a), 1 = "best" (np_b); game
   // i starts with turn i % 2 (evaluate, :597-599)
-  // (the parameter blocks live in device memory: a reference chosen between two
-  // by-value kernel arguments would copy both to scratch)
-  const NetParams& np = *((pp.arena && (((pp.game_base + g) + mv) & 1)) ? np_b : np_a);
+  // (field by field: a reference chosen between the two by-value kernel
+  // arguments would copy both to scratch)
+  const NetParams np = select_params(pp.arena && (((pp.game_base + g) + mv) & 1), np_b, np_a);
   const size_t rec = (size_t)g * E.max_moves + mv;
   for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
     E.rec_stones[rec * G::CELLS + c] = sm.stone[c];
