@@ -313,6 +313,8 @@ struct mzgo_engine {
     sp.variant = cfg.search_variant;
     sp.factored = cfg.direct_dynamics ? 0 : 1;
     sp.seed = cfg.seed;
+    sp.helpers = 0;
+    sp.net = 0;
     return sp;
   }
 };
@@ -441,6 +443,7 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     chk(e->alloc(&E.path, G * (n1 + 1)));
     chk(e->alloc(&E.nodes, G));
     chk(e->alloc(&E.nact, G * n1));
+    chk(e->alloc(&E.jobs, (size_t)G * job_bytes(A)));
     chk(e->alloc(&E.rec_stones, G * M * CELLS));
     chk(e->alloc(&E.rec_invd, G * M * CELLS));
     chk(e->alloc(&E.rec_flags, G * M));
@@ -648,6 +651,21 @@ int mzgo_selfplay_reset(mzgo_engine* e, int epoch, void* stream) {
   return MZGO_OK;
 }
 
+// k_selfplay_move; boards whose batch expansions stream Y from L2 (19x19) get
+// helper workgroups, 3 per game by default (MZGO_HELPERS_PER_GAME), with the
+// job slots zeroed before the launch (batch_expand_shared)
+static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayParams& pp, hipStream_t s) {
+  SearchParams sp = e->search_params();
+  if (e->ks->shared_batches) {
+    int per = 3;
+    if (const char* v = getenv("MZGO_HELPERS_PER_GAME")) per = atoi(v);
+    sp.helpers = per > 0 ? per * e->G : 0;
+    HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
+  }
+  HIPCHK(e->ks->selfplay_move(e->np, np_b, sp, pp, e->E, e->G, s));
+  return MZGO_OK;
+}
+
 int mzgo_selfplay_move(mzgo_engine* e, void* stream) { return mzgo_selfplay_moves(e, 1, stream); }
 
 int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
@@ -677,8 +695,7 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
     }
     return MZGO_OK;
   }
-  HIPCHK(e->ks->selfplay_move(e->np, e->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
-  return MZGO_OK;
+  return launch_selfplay(e, e->np, pp, (hipStream_t)stream);
 }
 
 int mzgo_arena_move(mzgo_engine* e, mzgo_engine* opponent, void* stream) {
@@ -704,8 +721,7 @@ int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* str
   pp.noise = e->noise;
   pp.arena = 1;
   pp.moves = moves;
-  HIPCHK(e->ks->selfplay_move(e->np, opponent->np, e->search_params(), pp, e->E, e->G, (hipStream_t)stream));
-  return MZGO_OK;
+  return launch_selfplay(e, opponent->np, pp, (hipStream_t)stream);
 }
 
 int mzgo_tower_timing(mzgo_engine* e, int enable, double* tower_ms, int64_t* towers) {

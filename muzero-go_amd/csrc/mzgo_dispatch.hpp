@@ -9,6 +9,7 @@ struct KernelSet {
   int N, C;
   size_t lds_bytes;
   int rep_scratch;   // floats of HBM scratch per initial_inference item (strip boards), else 0
+  int shared_batches;  // 1: the batch expansions stream Y from L2 and take helper workgroups (19x19)
   hipError_t (*initial_inference)(const NetParams&, const float* obs, int B, float* lat, float* val,
                                   float* logits, float* scratch, hipStream_t);
   hipError_t (*recurrent_inference)(const NetParams&, const float* lat, const int64_t* act, int B,
@@ -63,11 +64,15 @@ struct Launch {
   }
   static hipError_t move(const NetParams& np, const NetParams& np_b, const SearchParams& sp,
                          const PlayParams& pp, const EngineArrays& E, int G, hipStream_t s) {
-    hipLaunchKernelGGL((k_selfplay_move<N, C>), dim3(G), dim3(Geo<N, C>::THREADS), 0, s, np, np_b, sp, pp, E);
+    hipLaunchKernelGGL((k_selfplay_move<N, C>), dim3(G + sp.helpers), dim3(Geo<N, C>::THREADS), 0, s, np, np_b, sp,
+                       pp, E);
     return hipGetLastError();
   }
   static KernelSet table() {
-    return KernelSet{N, C, sizeof(Smem<Geo<N, C>>), rep_needs_scratch<Geo<N, C>>() ? 64 * N * N : 0, &ii, &ri, &search, &breset, &bstep, &bplanes, &move};
+    typedef Geo<N, C> G;
+    return KernelSet{N, C, sizeof(Smem<G>), rep_needs_scratch<G>() ? 64 * N * N : 0,
+                     Smem<G>::GLOBAL_Y ? 1 : 0, &ii, &ri, &search, &breset, &bstep, &bplanes,
+                     &move};
   }
 };
 

@@ -67,6 +67,7 @@ struct EngineArrays {
   int* game_len;         // [G]
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
+  unsigned char* jobs;   // [G][job_bytes(A)] batch-expansion jobs shared with helper workgroups
   unsigned long long* counters;  // [4] 0: simulations run, 1: moves played, 2: games finished,
                                  //     3: dynamics convs run (factored: one per new parent)
   unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
@@ -109,6 +110,7 @@ struct Smem {
                 "the batched expansion's LDS must fit the conv staging it overlays");
   __device__ float* heads() { return u.hp; }
   __device__ float* ulds() { return u.in; }             // the union as scratch
+  static constexpr bool GLOBAL_Y = ExpandLds<G, G::CINMAX * G::CPAD>::GLOBAL_Y;
   static constexpr int HEAD_PARTS = ConvShape<G::C>::NCOG;
 };
 
@@ -141,6 +143,7 @@ struct Smem<G, true> {
                 "the batched expansion's LDS must fit the Winograd input it overlays");
   __device__ float* heads() { return STRIPS ? hfin : u.x.hp; }
   __device__ float* ulds() { return u.v; }              // the union as scratch
+  static constexpr bool GLOBAL_Y = ExpandLds<G, Wino<G>::template v_floats<G::CINMAX>()>::GLOBAL_Y;
   static constexpr int HEAD_PARTS = STRIPS ? 1 : G::C / 16;
 };
 
@@ -389,6 +392,216 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
     for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
 }
 
+// ---------------------------------------------------------------------------
+// Batch expansions shared with helper workgroups (GLOBAL_Y boards, 19x19).
+// A 19x19 game has one workgroup, so with 64 games 192 CUs would idle; the
+// self-play launch adds sp.helpers workgroups (3 per game), and a game's
+// batch expansion (up to A children, each an L2 stream of its leaf's Y)
+// becomes a job that its workgroup and its helpers share: the game's
+// workgroup publishes the job (the actions, the leaf, the children's node
+// ids), every workgroup claims children a round of WAVES at a time, computes
+// them exactly as batch_expand does (the same function per child) and writes
+// the rows and backup values to HBM; the game's workgroup waits until all B
+// are done, then continues.  It never waits for a helper to START (it claims
+// children itself until none are left), so nothing depends on helpers being
+// resident.  Hand-offs: agent-scope release / relaxed flag / agent-scope
+// acquire (cdna_hip_programming.md Guideline 16); claims: a CAS on one
+// 64-bit word (batch number << 32 | next child), so a claim of a finished
+// batch fails.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int job_bytes(int A) {
+  return 256 + (A * 4 + 255) / 256 * 256 + (A * 8 + 255) / 256 * 256 + (A + 255) / 256 * 256;
+}
+constexpr unsigned kJobExit = 0xFFFFFFFFu;
+struct JobView {
+  unsigned char* base;
+  __device__ unsigned long long* claim() const { return reinterpret_cast<unsigned long long*>(base); }
+  __device__ unsigned* seq() const { return reinterpret_cast<unsigned*>(base + 64); }
+  __device__ unsigned* done() const { return reinterpret_cast<unsigned*>(base + 128); }
+  __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }   // B, nid0, leaf, net
+  __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
+  __device__ int* acts() const { return reinterpret_cast<int*>(base + 256); }
+  __device__ double* bv(int A) const { return reinterpret_cast<double*>(base + 256 + (A * 4 + 255) / 256 * 256); }
+  // the root's valid mask (child_priors reads it)
+  __device__ uint8_t* valid(int A) const {
+    return base + 256 + (A * 4 + 255) / 256 * 256 + (A * 8 + 255) / 256 * 256;
+  }
+};
+template <class G>
+__device__ __forceinline__ JobView job_of(const EngineArrays& E, int g) {
+  return JobView{E.jobs + (size_t)g * job_bytes(G::A)};
+}
+
+// One child of a batch by ONE wave (batch_expand's per-child work): E[a]
+// into W.ew, expand_wave over Y, the heads, the child's prior row (LAZY: its
+// logits) and child row; returns the backup value r + discount * v (every lane).
+template <class G, bool LAZY>
+__device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                               const TreeView& TV, const float* yg, const ExpandPlan<G>& plan,
+                                               int a, int nid) {
+  auto& L = sm.u.f;
+  typedef decltype(sm.u.f) XL;
+  const int lane = lane_id_local();
+  auto& W = L.wv[__builtin_amdgcn_readfirstlane(wave_id())];
+  constexpr int E4N = 9 * G::C / 4;
+  f32x4* ewl = reinterpret_cast<f32x4*>(W.ew);
+  const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
+  for (int i = lane; i < E4N; i += 64) ewl[i] = e4[i];
+  wave_lds_sync();
+  float rsum, vsum;
+  if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+  else expand_wave<G, XL::PROW>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
+  wave_lds_sync();
+  float r, v, x[G::AP];
+  heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
+  policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
+  if constexpr (LAZY) {
+    float* prow = TV.prior + (size_t)nid * G::A;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
+    if (lane == 0) atomicOr(&sm.t.rawp[nid >> 5], 1u << (nid & 31));
+  } else {
+    int* crow = TV.child + (size_t)nid * G::A;
+    for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+    child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
+  }
+  wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
+  return (double)r + sp.discount * (double)v;
+}
+
+// The children of job J (batch bseq, B children, node ids nid0 + k, actions
+// in L.acts) a round of WAVES at a time, claimed by CAS; each child's backup
+// value goes to J.bv (HBM).  Returns this workgroup's count.  All threads.
+template <class G, bool LAZY>
+__device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                          const TreeView& TV, const float* yg, const JobView& J, unsigned bseq,
+                                          int B, int nid0) {
+  auto& L = sm.u.f;
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+  ExpandPlan<G> plan;
+  plan.init();
+  double* bvg = J.bv(G::A);
+  int mine = 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int c0 = -1;
+      unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (;;) {                                     // (a failed CAS means another claim succeeded)
+        if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFFFFFu) >= B) break;
+        if (__hip_atomic_compare_exchange_strong(J.claim(), &c, c + G::WAVES, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          c0 = (int)(c & 0xFFFFFFFFu);
+          break;
+        }
+      }
+      sm.bc[1] = c0;
+    }
+    __syncthreads();
+    const int c0 = sm.bc[1];
+    __syncthreads();                                 // (bc[1] is rewritten by the next claim)
+    if (c0 < 0) break;
+    const int k = c0 + wave;
+    if (k < B) {
+      const int a = __builtin_amdgcn_readfirstlane(L.acts[k]);
+      const double bv = expand_child<G, LAZY>(sm, np, sp, TV, yg, plan, a, nid0 + k);
+      if (lane_id_local() == 0) bvg[k] = bv;
+    }
+    mine += (B - c0 < G::WAVES ? B - c0 : G::WAVES);
+  }
+  return mine;
+}
+
+// The game's workgroup: batch_expand over the job machinery (B children of
+// leaf `leaf` whose Y is yg, actions in L.acts, node ids nid0 + k); L.bv
+// gets every child's backup value.
+template <class G, bool LAZY>
+__device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
+                                                    const EngineArrays& E, int g, const TreeView& TV, int B,
+                                                    int nid0, int leaf, int net, const float* yg) {
+  auto& L = sm.u.f;
+  const JobView J = job_of<G>(E, g);
+  // batch numbers are unique within a launch (the host zeroes the jobs before it)
+  const unsigned bseq = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  // the job: actions, geometry; then (release: these and the leaf's Y, written
+  // by this workgroup's conv, reach the helpers) the batch number
+  for (int k = threadIdx.x; k < B; k += G::THREADS) J.acts()[k] = L.acts[k];
+  for (int a = threadIdx.x; a < G::A; a += G::THREADS) J.valid(G::A)[a] = sm.t.valid[a];
+  if (threadIdx.x == 0) {
+    int* info = J.info();
+    info[0] = B; info[1] = nid0; info[2] = leaf; info[3] = net;
+    *J.pass_prior() = sm.t.pass_prior;
+    __hip_atomic_store(J.done(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(J.seq(), bseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0);
+  // every child done (the helpers' adds come after their release)
+  if (threadIdx.x == 0) {
+    unsigned d = __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
+    while (d < (unsigned)B) {
+      __builtin_amdgcn_s_sleep(4);
+      d = __hip_atomic_load(J.done(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const double* bvg = J.bv(G::A);
+  for (int k = threadIdx.x; k < B; k += G::THREADS) L.bv[k] = bvg[k];
+  __syncthreads();
+}
+
+// A helper workgroup of game g (k_selfplay_move's blocks past the games):
+// jobs until the game's workgroup posts kJobExit (or none comes for ~seconds).
+template <class G>
+__device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, const NetParams& np_b,
+                                            const SearchParams& sp, const EngineArrays& E, int g) {
+  const JobView J = job_of<G>(E, g);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  float* pool = pool_of<G>(E, g);
+  unsigned last = 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 26); ++spins) {
+        __builtin_amdgcn_s_sleep(8);
+        s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (s == last || s == 0) s = kJobExit;           // (bounded wait: give up)
+      if (s != kJobExit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sm.bc[2] = (int)s;
+    }
+    __syncthreads();
+    const unsigned s = (unsigned)sm.bc[2];
+    if (s == kJobExit) return;
+    last = s;
+    const int* info = J.info();
+    const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3];
+    const NetParams np = select_params(net != 0, np_b, np_a);
+    for (int k = threadIdx.x; k < B; k += G::THREADS) sm.u.f.acts[k] = J.acts()[k];
+    for (int a = threadIdx.x; a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
+    if (threadIdx.x == 0) sm.t.pass_prior = *J.pass_prior();
+    stage_head_scalars(np.hs, sm.t.hsc);
+    load_y<G>(sm, nullptr, np.head_w);                 // (GLOBAL_Y: the head weights only)
+    __syncthreads();
+    const float* yg = pool + (size_t)leaf * G::C * G::CS;
+    const int mine = job_rounds<G, false>(sm, np, sp, TV, yg, J, s, B, nid0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row and value stores
+    __syncthreads();
+    if (threadIdx.x == 0 && mine > 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // dst[0] = w0, dst[k + 1] = dst[k] + (neg ? -v[k] : v[k]) for k < B: the
 // sequential f64 sums (lane 0), 8 at a time without branches, the next 8
 // loads in flight: v is read up to 15 and dst written up to 7 entries past B
@@ -428,8 +641,8 @@ __device__ __forceinline__ double prefix_sums(double w0, const double* __restric
 // same node for node.  Returns K (0: no batch).
 template <class G, class Acc>
 __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
-                                          const TreeView& TV, Acc& T, float* pool, float* scratch, int* nact,
-                                          uint64_t key, Stamp* st = nullptr) {
+                                          const EngineArrays& E, int g, const TreeView& TV, Acc& T, float* pool,
+                                          float* scratch, int* nact, uint64_t key, Stamp* st = nullptr) {
   auto& L = sm.u.f;
   if constexpr (!decltype(sm.u.f)::BATCH) {
     return 0;
@@ -473,7 +686,12 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       }
     }
     if (wave_id() == 0) pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
-    batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, pool, st);
+    if (decltype(sm.u.f)::GLOBAL_Y && sp.helpers > 0) {
+      __syncthreads();                                // every pick made
+      batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, K, 1, 0, sp.net, pool);
+    } else {
+      batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, pool, st);
+    }
     __syncthreads();
     if (st) st->lap(62);
     if (wave_id() == 0) {
@@ -851,7 +1069,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   Stamp st(E.stamps);
   int sim = 0;
   if (factored) {
-    sim = root_batch<G, Acc>(sm, np, sp, TV, T, pool, scratch, nact, key, &st);
+    sim = root_batch<G, Acc>(sm, np, sp, E, g, TV, T, pool, scratch, nact, key, &st);
     nodes += sim;
     convs += sim > 0 ? 1 : 0;
     st.lap(4);
@@ -927,7 +1145,12 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1);
           st.lap(71);
         }
-        batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
+        if (decltype(sm.u.f)::GLOBAL_Y && sp.helpers > 0) {
+          __syncthreads();                            // every pick made
+          batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf);
+        } else {
+          batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
+        }
         __syncthreads();
         st.lap(5);
         if (depth <= kVerifyMaxDepth) {
@@ -1384,9 +1607,20 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                              SearchParams sp, PlayParams pp, EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
-  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
+  // blocks past the games are helper workgroups (batch_expand_shared): helper h
+  // serves game h % games (the same XCD under round-robin dispatch)
+  const int games = gridDim.x - sp.helpers;
+  if ((int)blockIdx.x >= games) {
+    if constexpr (decltype(sm.u.f)::GLOBAL_Y) helper_loop<G>(sm, np_a, np_b, sp, E, (blockIdx.x - games) % games);
+    return;
+  }
   const int g = blockIdx.x;
-  if (E.status[g] != 0) return;
+  auto release_helpers = [&]() {
+    if (sp.helpers > 0 && threadIdx.x == 0)
+      __hip_atomic_store(job_of<G>(E, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (E.status[g] != 0) { release_helpers(); return; }
+  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   BoardMeta m;
   load_board<G>(sm, E, g, m);
   // pp.moves moves of this game in one launch (the board stays in LDS between
@@ -1423,7 +1657,9 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #ifdef MZGO_STAMPS
   tm[1] = __builtin_amdgcn_s_memtime();
 #endif
-  run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
+  SearchParams spm = sp;
+  spm.net = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? 1 : 0;
+  run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
                 tm ? tm + 2 : nullptr);
 #ifdef MZGO_STAMPS
   tm[4] = __builtin_amdgcn_s_memtime();
@@ -1482,6 +1718,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if (over) break;
   __syncthreads();                               // this move's LDS reads before the next move's writes
   }
+  release_helpers();
 }
 
 }  // namespace mzgo

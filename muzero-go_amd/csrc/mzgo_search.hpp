@@ -28,6 +28,8 @@ struct SearchParams {
   int variant;              // 0: self_play.py MCTS, 1: main.py MCTS (main.py:246-368)
   int factored;             // 1: factored dynamics expansion (mzgo_expand.hpp), 0: a conv per simulation
   uint64_t seed;
+  int helpers;              // helper workgroups sharing the batch expansions (GLOBAL_Y boards; 0: none)
+  int net;                  // k_selfplay_move: the network of this move (arena: 1 = np_b), for the helpers
 };
 
 // One game's tree (global memory).  Node 0 is the root; node ids grow by one
