@@ -565,16 +565,14 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
 // picks the r_i-th (ascending) of the n - i still unexpanded ones (bitmask m),
 // r_i = randbelow(draw(key, TAG_SELECT, sim0 + i), n - i) -- select_leaf's
 // random.choice (self_play.py:283-287) replayed.  The draws are made in
-// parallel (lane i = lane + 64 q); then, pick by pick, every element keeps
-// its rank among the remaining ones (lane a = lane + 64 q), the pick is the
-// remaining element of rank r_i (a ballot), and the ranks above it drop by
-// one.  out[i0 + i] (LDS) gets the actions; *progress (LDS, if given) is
-// published after the first `head` picks and every 12 after.  Wave-level.
+// parallel (lane i = lane + 64 q); then, pick by pick, the remaining element
+// of rank r_i is found in the remaining set's bitmask with scalar popcounts
+// and removed.  out[i0 + i] (LDS) gets the actions; *progress (LDS, if given)
+// is published after the first `head` picks and every 12 after.  Wave-level.
 template <class G>
 struct PickSeq {
   uint32_t r[G::AP];       // lane i = lane + 64 q: simulation i's rank among the remaining
-  uint64_t rem[G::AP];     // the remaining elements (wave-uniform)
-  uint32_t rank[G::AP];    // lane a = lane + 64 j: element a's rank among them
+  uint64_t rem[G::AP];     // the remaining elements (wave-uniform: scalar registers)
   __device__ __forceinline__ PickSeq() {}
   __device__ __forceinline__ PickSeq(const uint64_t (&m)[G::AP], int n, int count, uint64_t key, int sim0) {
     const int lane = lane_id_local();
@@ -589,33 +587,34 @@ struct PickSeq {
       const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m[j] >> 32));
       rem[j] = ((uint64_t)hi << 32) | lo;
     }
-    uint32_t below = 0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      rank[j] = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(rem[j] >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)rem[j], 0u));
-      below += (uint32_t)__popcll(rem[j]);
-    }
   }
-  // pick i (in order i = 0, 1, ...): the remaining element of rank r_i
+  // pick i (in order i = 0, 1, ...): the remaining element of rank r_i, by
+  // scalar popcounts (the word, then a binary search inside it)
   __device__ __forceinline__ int pick(int i) {
-    const int lane = lane_id_local();
-    uint32_t ri = 0;
+    uint32_t k = 0;
 #pragma unroll
     for (int q = 0; q < G::AP; ++q)
-      if ((i >> 6) == q) ri = (uint32_t)__builtin_amdgcn_readlane((int)r[q], i & 63);
-    int a = 0;
-    bool found = false;
+      if ((i >> 6) == q) k = (uint32_t)__builtin_amdgcn_readlane((int)r[q], i & 63);
+    int w = 0;
+    uint64_t x = rem[0];
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) {
-      const uint64_t hit = __ballot(rank[j] == ri) & rem[j];
-      if (!found && hit) { a = 64 * j + __ffsll((long long)hit) - 1; found = true; }
+      const uint32_t c = (uint32_t)__builtin_popcountll(rem[j]);
+      if (w == j) {
+        if (k < c || j == G::AP - 1) { x = rem[j]; }
+        else { k -= c; w = j + 1; }
+      }
     }
+    int pos = 0;
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      if ((a >> 6) == j) rem[j] &= ~(1ull << (a & 63));
-      rank[j] -= (lane + 64 * j > a) ? 1u : 0u;
+    for (int h = 32; h >= 1; h >>= 1) {
+      const uint32_t c = (uint32_t)__builtin_popcountll(x & ((1ull << h) - 1));
+      if (k >= c) { k -= c; x >>= h; pos += h; }
     }
+    const int a = 64 * w + pos;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (w == j) rem[j] &= ~(1ull << pos);
     return a;
   }
 };
