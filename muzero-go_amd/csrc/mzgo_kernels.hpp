@@ -418,7 +418,7 @@ struct JobView {
   __device__ unsigned long long* claim() const { return reinterpret_cast<unsigned long long*>(base); }
   __device__ unsigned* seq() const { return reinterpret_cast<unsigned*>(base + 64); }
   __device__ unsigned* done() const { return reinterpret_cast<unsigned*>(base + 128); }
-  __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }   // B, nid0, leaf, net
+  __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }   // B, nid0, leaf, net, kind
   __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
   __device__ int* acts() const { return reinterpret_cast<int*>(base + 256); }
   __device__ double* bv(int A) const { return reinterpret_cast<double*>(base + 256 + (A * 4 + 255) / 256 * 256); }
@@ -430,6 +430,106 @@ struct JobView {
 template <class G>
 __device__ __forceinline__ JobView job_of(const EngineArrays& E, int g) {
   return JobView{E.jobs + (size_t)g * job_bytes(G::A)};
+}
+
+// the parent convs and batch expansions go through jobs: 19x19 (Y streamed
+// from L2, strip convs) with helper workgroups in the launch
+template <class G>
+__device__ __forceinline__ bool shared_jobs(const SearchParams& sp) {
+  if constexpr (Smem<G>::GLOBAL_Y && G::WINO) return Wino<G>::NSTRIP > 1 && sp.helpers > 0;
+  else return false;
+}
+
+// A job's batch number (unique within a launch: the host zeroes the jobs
+// before it) with the claim word and the done counter reset for it.  Thread 0.
+__device__ __forceinline__ unsigned job_begin(const JobView& J) {
+  const unsigned bseq = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(J.done(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return bseq;
+}
+// every store of the workgroup drained, then (release) the batch number.  All threads.
+__device__ __forceinline__ void job_publish(const JobView& J, unsigned bseq) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(J.seq(), bseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// this workgroup's `mine` units added; wait until all `total` are done
+// (every helper adds after its release), then acquire.  All threads.
+__device__ __forceinline__ void job_wait(const JobView& J, int mine, int total) {
+  if (threadIdx.x == 0) {
+    unsigned d = __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
+    while (d < (unsigned)total) {
+      __builtin_amdgcn_s_sleep(4);
+      d = __hip_atomic_load(J.done(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+// claim the next unit of batch bseq (of total): -1 when none is left.  Thread 0
+// claims, the workgroup gets it through LDS.  All threads.
+template <class G>
+__device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned bseq, int total, int step) {
+  if (threadIdx.x == 0) {
+    int c0 = -1;
+    unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {                                       // (a failed CAS means another claim succeeded)
+      if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFFFFFu) >= total) break;
+      if (__hip_atomic_compare_exchange_strong(J.claim(), &c, c + step, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        c0 = (int)(c & 0xFFFFFFFFu);
+        break;
+      }
+    }
+    sm.bc[1] = c0;
+  }
+  __syncthreads();
+  const int c0 = sm.bc[1];
+  __syncthreads();                                   // (bc[1] is rewritten by the next claim)
+  return c0;
+}
+
+// The dynamics conv of a parent as a job (19x19: 5 row strips, each strip
+// independent given the input): src (the rebuilt latent, [C][CS]) -> dst
+// (its Y, [CELLS][C]); strips claimed one at a time.  Returns this
+// workgroup's strips.  All threads.
+template <class G>
+__device__ __forceinline__ int conv_strips(Smem<G>& sm, const NetParams& np, const JobView& J, unsigned bseq,
+                                           const float* src, float* dst) {
+  int mine = 0;
+  if constexpr (G::WINO) {
+    for (int s; (s = job_claim(sm, J, bseq, Wino<G>::NSTRIP, 1)) >= 0; ++mine) {
+      wino_input<G, G::C>(sm.u.v, sm.raw, src, G::CS, nullptr, s);
+      wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
+                                         dst, G::CS, G::CS, nullptr, s);
+    }
+  }
+  __syncthreads();
+  return mine;
+}
+
+// The game's workgroup: the parent's conv over the job machinery (src and
+// dst in HBM; dst = the pool slot of node `leaf`).  All threads; returns
+// synchronised with dst complete and acquired.
+template <class G>
+__device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, const EngineArrays& E, int g,
+                                            int leaf, int net, const float* src, float* dst) {
+  const JobView J = job_of<G>(E, g);
+  const unsigned bseq = job_begin(J);
+  if (threadIdx.x == 0) {
+    int* info = J.info();
+    info[0] = Wino<G>::NSTRIP; info[1] = 0; info[2] = leaf; info[3] = net; info[4] = 1;
+  }
+  job_publish(J, bseq);                              // (the rebuilt latent src reaches the helpers)
+  const int mine = conv_strips<G>(sm, np, J, bseq, src, dst);
+  job_wait(J, mine, Wino<G>::NSTRIP);
 }
 
 // One child of a batch by ONE wave (batch_expand's per-child work): E[a]
@@ -484,22 +584,7 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
   double* bvg = J.bv(G::A);
   int mine = 0;
   for (;;) {
-    if (threadIdx.x == 0) {
-      int c0 = -1;
-      unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (;;) {                                     // (a failed CAS means another claim succeeded)
-        if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFFFFFu) >= B) break;
-        if (__hip_atomic_compare_exchange_strong(J.claim(), &c, c + G::WAVES, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          c0 = (int)(c & 0xFFFFFFFFu);
-          break;
-        }
-      }
-      sm.bc[1] = c0;
-    }
-    __syncthreads();
-    const int c0 = sm.bc[1];
-    __syncthreads();                                 // (bc[1] is rewritten by the next claim)
+    const int c0 = job_claim(sm, J, bseq, B, G::WAVES);
     if (c0 < 0) break;
     const int k = c0 + wave;
     if (k < B) {
@@ -521,37 +606,19 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
                                                     int nid0, int leaf, int net, const float* yg) {
   auto& L = sm.u.f;
   const JobView J = job_of<G>(E, g);
-  // batch numbers are unique within a launch (the host zeroes the jobs before it)
-  const unsigned bseq = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  // the job: actions, geometry; then (release: these and the leaf's Y, written
-  // by this workgroup's conv, reach the helpers) the batch number
+  const unsigned bseq = job_begin(J);
+  // the job: actions, geometry, the root's mask; then (release: these and
+  // the leaf's Y reach the helpers) the batch number
   for (int k = threadIdx.x; k < B; k += G::THREADS) J.acts()[k] = L.acts[k];
   for (int a = threadIdx.x; a < G::A; a += G::THREADS) J.valid(G::A)[a] = sm.t.valid[a];
   if (threadIdx.x == 0) {
     int* info = J.info();
-    info[0] = B; info[1] = nid0; info[2] = leaf; info[3] = net;
+    info[0] = B; info[1] = nid0; info[2] = leaf; info[3] = net; info[4] = 0;
     *J.pass_prior() = sm.t.pass_prior;
-    __hip_atomic_store(J.done(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(J.seq(), bseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  job_publish(J, bseq);
   const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0);
-  // every child done (the helpers' adds come after their release)
-  if (threadIdx.x == 0) {
-    unsigned d = __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
-    while (d < (unsigned)B) {
-      __builtin_amdgcn_s_sleep(4);
-      d = __hip_atomic_load(J.done(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+  job_wait(J, mine, B);
   const double* bvg = J.bv(G::A);
   for (int k = threadIdx.x; k < B; k += G::THREADS) L.bv[k] = bvg[k];
   __syncthreads();
@@ -583,8 +650,19 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     if (s == kJobExit) return;
     last = s;
     const int* info = J.info();
-    const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3];
+    const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3], kind = info[4];
     const NetParams np = select_params(net != 0, np_b, np_a);
+    if (kind == 1) {                                   // a parent's conv
+      const int mine = conv_strips<G>(sm, np, J, s, pool + (size_t)(E.S + 1) * G::C * G::CS,
+                                      pool + (size_t)leaf * G::C * G::CS);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0 && mine > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
     for (int k = threadIdx.x; k < B; k += G::THREADS) sm.u.f.acts[k] = J.acts()[k];
     for (int a = threadIdx.x; a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
     if (threadIdx.x == 0) sm.t.pass_prior = *J.pass_prior();
@@ -664,8 +742,12 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     // the root's conv Y (its latent is in the scratch slot), then Y and the
     // head weights into LDS.  The conv overwrites the whole union, so the
     // batch's LDS buffers are filled only after it.
-    latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
-                                        nullptr);
+    if (shared_jobs<G>(sp)) {
+      conv_shared<G>(sm, np, E, g, 0, sp.net, scratch, pool);
+    } else {
+      latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
+                                          nullptr);
+    }
     __syncthreads();
     if (st) st->lap(60);
     load_y<G>(sm, pool, np.head_w);
@@ -686,7 +768,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       }
     }
     if (wave_id() == 0) pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
-    if (decltype(sm.u.f)::GLOBAL_Y && sp.helpers > 0) {
+    if (shared_jobs<G>(sp)) {
       __syncthreads();                                // every pick made
       batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, K, 1, 0, sp.net, pool);
     } else {
@@ -1109,8 +1191,12 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
                          sm.ulds());
         }
         st.lap(81);
-        latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS, G::CS,
-                                            nullptr, &st);
+        if (shared_jobs<G>(sp)) {
+          conv_shared<G>(sm, np, E, g, leaf, sp.net, scratch, yleaf);
+        } else {
+          latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS,
+                                              G::CS, nullptr, &st);
+        }
         __syncthreads();                                 // Y stores before the expansion reads them
         st.lap(82);
         yc = -1;                                         // the conv overwrote the LDS copy
@@ -1145,7 +1231,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1);
           st.lap(71);
         }
-        if (decltype(sm.u.f)::GLOBAL_Y && sp.helpers > 0) {
+        if (shared_jobs<G>(sp)) {
           __syncthreads();                            // every pick made
           batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf);
         } else {
@@ -1611,7 +1697,10 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   // serves game h % games (the same XCD under round-robin dispatch)
   const int games = gridDim.x - sp.helpers;
   if ((int)blockIdx.x >= games) {
-    if constexpr (decltype(sm.u.f)::GLOBAL_Y) helper_loop<G>(sm, np_a, np_b, sp, E, (blockIdx.x - games) % games);
+    if constexpr (Smem<G>::GLOBAL_Y && G::WINO) {
+      wino_raw_zero<G>(sm.raw);                          // the conv strips' zero halo
+      helper_loop<G>(sm, np_a, np_b, sp, E, (blockIdx.x - games) % games);
+    }
     return;
   }
   const int g = blockIdx.x;
