@@ -1228,7 +1228,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         for (int j = 0; j < G::AP; ++j)
           if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
         if (wave_id() == 0) {
-          pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1);
+          pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1, &st);
           st.lap(71);
         }
         if (shared_jobs<G>(sp)) {

@@ -588,42 +588,46 @@ struct PickSeq {
       rem[j] = ((uint64_t)hi << 32) | lo;
     }
   }
-  // pick i (in order i = 0, 1, ...): the remaining element of rank r_i, by
-  // scalar popcounts (the word, then a binary search inside it)
+  // pick i (in order i = 0, 1, ...): the remaining element of rank r_i: the
+  // word from the words' prefix popcounts (scalar, no branches), the bit by a
+  // ballot of the lanes' mbcnt ranks inside it
   __device__ __forceinline__ int pick(int i) {
     uint32_t k = 0;
 #pragma unroll
     for (int q = 0; q < G::AP; ++q)
       if ((i >> 6) == q) k = (uint32_t)__builtin_amdgcn_readlane((int)r[q], i & 63);
-    int w = 0;
+    uint32_t pre = 0, w = 0, base = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP - 1; ++j) {
+      pre += (uint32_t)__builtin_popcountll(rem[j]);
+      const bool past = k >= pre;                    // rank k lies beyond word j
+      w += past ? 1u : 0u;
+      base = past ? pre : base;
+    }
+    k -= base;
     uint64_t x = rem[0];
 #pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const uint32_t c = (uint32_t)__builtin_popcountll(rem[j]);
-      if (w == j) {
-        if (k < c || j == G::AP - 1) { x = rem[j]; }
-        else { k -= c; w = j + 1; }
-      }
-    }
-    int pos = 0;
+    for (int j = 1; j < G::AP; ++j) x = w == (uint32_t)j ? rem[j] : x;
+    // the k-th set bit of x: the lane holding a set bit with k set bits below it
+    const uint32_t lane = (uint32_t)lane_id_local();
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(x >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)x, 0u));
+    const uint32_t pos = (uint32_t)__builtin_ctzll(__ballot(((x >> lane) & 1ull) && below == k));
 #pragma unroll
-    for (int h = 32; h >= 1; h >>= 1) {
-      const uint32_t c = (uint32_t)__builtin_popcountll(x & ((1ull << h) - 1));
-      if (k >= c) { k -= c; x >>= h; pos += h; }
-    }
-    const int a = 64 * w + pos;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (w == j) rem[j] &= ~(1ull << pos);
-    return a;
+    for (int j = 0; j < G::AP; ++j) rem[j] &= w == (uint32_t)j ? ~(1ull << pos) : ~0ull;
+    return (int)(64 * w + pos);
   }
+
 };
 
 template <class G>
 __device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
-                                              int sim0, int* out, int* progress = nullptr, int head = 1) {
+                                              int sim0, int* out, int* progress = nullptr, int head = 1,
+                                              Stamp* st = nullptr) {
   const int lane = lane_id_local();
+  const unsigned long long t0 = st ? st->now() : 0;
   PickSeq<G> ps(m, n, count, key, sim0);
+  const unsigned long long t1 = st ? st->now() : 0;
+  if (st) st->wave_add(66, t1 - t0);
   int next_pub = head < count ? head : count;
   for (int i = 0; i < count; ++i) {
     const int a = ps.pick(i);
@@ -634,6 +638,7 @@ __device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n,
       next_pub = next_pub + 12 < count ? next_pub + 12 : count;
     }
   }
+  if (st) st->wave_add(67, st->now() - t1);
 }
 
 // PUCT over the eligible, all expanded children elig (self_play.py:290-308;
