@@ -418,6 +418,7 @@ struct JobView {
   __device__ unsigned long long* claim() const { return reinterpret_cast<unsigned long long*>(base); }
   __device__ unsigned* seq() const { return reinterpret_cast<unsigned*>(base + 64); }
   __device__ unsigned* done() const { return reinterpret_cast<unsigned*>(base + 128); }
+  __device__ unsigned* picked() const { return reinterpret_cast<unsigned*>(base + 160); }   // actions out so far
   __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }   // B, nid0, leaf, net, kind
   __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
   __device__ int* acts() const { return reinterpret_cast<int*>(base + 256); }
@@ -476,12 +477,21 @@ __device__ __forceinline__ void job_wait(const JobView& J, int mine, int total) 
 // claim the next unit of batch bseq (of total): -1 when none is left.  Thread 0
 // claims, the workgroup gets it through LDS.  All threads.
 template <class G>
-__device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned bseq, int total, int step) {
+__device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned bseq, int total, int step,
+                                         bool gated = false) {
   if (threadIdx.x == 0) {
     int c0 = -1;
     unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {                                       // (a failed CAS means another claim succeeded)
       if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFFFFFu) >= total) break;
+      if (gated) {                                   // the round's actions must be out (J.picked)
+        const unsigned need = (unsigned)min((int)(c & 0xFFFFFFFFu) + step, total);
+        if (__hip_atomic_load(J.picked(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+          __builtin_amdgcn_s_sleep(2);
+          c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          continue;
+        }
+      }
       if (__hip_atomic_compare_exchange_strong(J.claim(), &c, c + step, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
         c0 = (int)(c & 0xFFFFFFFFu);
@@ -576,7 +586,7 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
 template <class G, bool LAZY>
 __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                           const TreeView& TV, const float* yg, const JobView& J, unsigned bseq,
-                                          int B, int nid0) {
+                                          int B, int nid0, bool helper = false) {
   auto& L = sm.u.f;
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   ExpandPlan<G> plan;
@@ -584,11 +594,12 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
   double* bvg = J.bv(G::A);
   int mine = 0;
   for (;;) {
-    const int c0 = job_claim(sm, J, bseq, B, G::WAVES);
+    const int c0 = job_claim(sm, J, bseq, B, G::WAVES, helper);
     if (c0 < 0) break;
     const int k = c0 + wave;
     if (k < B) {
-      const int a = __builtin_amdgcn_readfirstlane(L.acts[k]);
+      const int a = __builtin_amdgcn_readfirstlane(
+          helper ? __hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : L.acts[k]);
       const double bv = expand_child<G, LAZY>(sm, np, sp, TV, yg, plan, a, nid0 + k);
       if (lane_id_local() == 0) bvg[k] = bv;
     }
@@ -603,20 +614,27 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
 template <class G, bool LAZY>
 __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                                     const EngineArrays& E, int g, const TreeView& TV, int B,
-                                                    int nid0, int leaf, int net, const float* yg) {
+                                                    int nid0, int leaf, int net, const float* yg,
+                                                    const uint64_t (&m)[G::AP], int n, int i0, uint64_t key,
+                                                    int sim0, Stamp* st = nullptr) {
   auto& L = sm.u.f;
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J);
-  // the job: actions, geometry, the root's mask; then (release: these and
-  // the leaf's Y reach the helpers) the batch number
-  for (int k = threadIdx.x; k < B; k += G::THREADS) J.acts()[k] = L.acts[k];
+  // the job first (geometry, the root's mask, the actions known already:
+  // i0 of them), then the picks: wave 0 streams the actions out in chunks
+  // (J.picked) while the helpers start on the first rounds
   for (int a = threadIdx.x; a < G::A; a += G::THREADS) J.valid(G::A)[a] = sm.t.valid[a];
   if (threadIdx.x == 0) {
     int* info = J.info();
     info[0] = B; info[1] = nid0; info[2] = leaf; info[3] = net; info[4] = 0;
     *J.pass_prior() = sm.t.pass_prior;
+    for (int k = 0; k < i0; ++k) __hip_atomic_store(J.acts() + k, L.acts[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(J.picked(), (unsigned)i0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   job_publish(J, bseq);
+  if (wave_id() == 0)
+    pick_sequence<G>(m, n, i0, B - i0, key, sim0, L.acts, nullptr, 12, st, J.acts(), J.picked());
+  __syncthreads();                                   // every pick made (in LDS too)
   const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0);
   job_wait(J, mine, B);
   const double* bvg = J.bv(G::A);
@@ -663,14 +681,13 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       }
       continue;
     }
-    for (int k = threadIdx.x; k < B; k += G::THREADS) sm.u.f.acts[k] = J.acts()[k];
     for (int a = threadIdx.x; a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
     if (threadIdx.x == 0) sm.t.pass_prior = *J.pass_prior();
     stage_head_scalars(np.hs, sm.t.hsc);
     load_y<G>(sm, nullptr, np.head_w);                 // (GLOBAL_Y: the head weights only)
     __syncthreads();
     const float* yg = pool + (size_t)leaf * G::C * G::CS;
-    const int mine = job_rounds<G, false>(sm, np, sp, TV, yg, J, s, B, nid0);
+    const int mine = job_rounds<G, false>(sm, np, sp, TV, yg, J, s, B, nid0, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row and value stores
     __syncthreads();
     if (threadIdx.x == 0 && mine > 0) {
@@ -767,11 +784,10 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         n += __popcll(el[j]);
       }
     }
-    if (wave_id() == 0) pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
     if (shared_jobs<G>(sp)) {
-      __syncthreads();                                // every pick made
-      batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, K, 1, 0, sp.net, pool);
+      batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, K, 1, 0, sp.net, pool, el, n, 0, key, 0);
     } else {
+      if (wave_id() == 0) pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
       batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, pool, st);
     }
     __syncthreads();
@@ -1227,14 +1243,15 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
 #pragma unroll
         for (int j = 0; j < G::AP; ++j)
           if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
-        if (wave_id() == 0) {
-          pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1, &st);
-          st.lap(71);
-        }
         if (shared_jobs<G>(sp)) {
-          __syncthreads();                            // every pick made
-          batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf);
+          batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf, um, nun - 1, 1, key,
+                                           sim + 1, &st);
+          st.lap(71);
         } else {
+          if (wave_id() == 0) {
+            pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1, &st);
+            st.lap(71);
+          }
           batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
         }
         __syncthreads();

@@ -619,22 +619,34 @@ struct PickSeq {
 
 };
 
+// gout / gprogress (HBM, optional): every published chunk of actions is also
+// stored write-through to gout (agent-scope relaxed stores, drained) and then
+// its count to *gprogress, for other workgroups (batch_expand_shared).
 template <class G>
 __device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
                                               int sim0, int* out, int* progress = nullptr, int head = 1,
-                                              Stamp* st = nullptr) {
+                                              Stamp* st = nullptr, int* gout = nullptr,
+                                              unsigned* gprogress = nullptr) {
   const int lane = lane_id_local();
   const unsigned long long t0 = st ? st->now() : 0;
   PickSeq<G> ps(m, n, count, key, sim0);
   const unsigned long long t1 = st ? st->now() : 0;
   if (st) st->wave_add(66, t1 - t0);
-  int next_pub = head < count ? head : count;
+  int next_pub = head < count ? head : count, gdone = 0;
   for (int i = 0; i < count; ++i) {
     const int a = ps.pick(i);
     if (lane == 0) out[i0 + i] = a;
-    if (progress && i + 1 == next_pub) {
+    if ((progress || gout) && i + 1 == next_pub) {
       wave_lds_sync();
-      if (lane == 0) __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (progress && lane == 0)
+        __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (gout) {
+        for (int k = gdone + lane; k <= i; k += 64)
+          __hip_atomic_store(gout + i0 + k, out[i0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(gprogress, (unsigned)(i0 + i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gdone = i + 1;
+      }
       next_pub = next_pub + 12 < count ? next_pub + 12 : count;
     }
   }
