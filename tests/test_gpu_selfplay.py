@@ -192,3 +192,29 @@ def test_multi_move_launches_equal_single_moves(chunks):
         assert a["length"] == b["length"] and a["final_reward"] == b["final_reward"]
         for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
             assert a[k].tobytes() == b[k].tobytes(), (g, k)
+
+
+@pytest.mark.parametrize("helpers", ["1", "3"])
+def test_helper_workgroups_do_not_change_records(helpers, monkeypatch):
+    """19x19: the helper workgroups that share each game's batch expansions
+    and parent convs (batch_expand_shared / conv_shared) leave every record
+    byte for byte as the game's workgroup alone produces it."""
+    import mzgo
+    from mzgo import distributed as mdist
+    N, G, S, M = 19, 16, 96, 12
+    net = _net(N)
+
+    def packed(h):
+        monkeypatch.setenv("MZGO_HELPERS_PER_GAME", h)
+        sp = mzgo.SelfPlay(net, G, S, seed=77)
+        sp.reset()
+        sp.move(M)
+        torch.cuda.synchronize()
+        return mdist.unpack(mdist.pack_engine(sp.engine).cpu().numpy(), G, sp.max_moves, N)
+
+    want, got = packed("0"), packed(helpers)
+    for g in range(G):
+        a, b = mdist.slot_records(got, g), mdist.slot_records(want, g)
+        assert a["length"] == b["length"]
+        for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
+            assert a[k].tobytes() == b[k].tobytes(), (g, k)
