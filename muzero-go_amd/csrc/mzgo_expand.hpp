@@ -261,7 +261,11 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
     f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
     for (int k = 0; k < X::PERL; ++k) {
+#ifdef MZGO_DIAG_YL1
+      y[k] = Y4[(p & 1) * 8 * X::C4 + 8 * k];          // (diagnostic: 16 cells, L1-resident)
+#else
       y[k] = Y4[p * 8 * X::C4 + 8 * k];
+#endif
       e[k] = E4[8 * k];
     }
     const bool live = G::CELLS % 8 == 0 || p < P - 1 || cg + 8 * p < G::CELLS;

@@ -410,7 +410,7 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
 // batch fails.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int job_bytes(int A) {
-  return 256 + (A * 4 + 255) / 256 * 256 + (A * 8 + 255) / 256 * 256 + (A + 255) / 256 * 256;
+  return 256 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256;
 }
 constexpr unsigned kJobExit = 0xFFFFFFFFu;
 struct JobView {
@@ -418,14 +418,16 @@ struct JobView {
   __device__ unsigned long long* claim() const { return reinterpret_cast<unsigned long long*>(base); }
   __device__ unsigned* seq() const { return reinterpret_cast<unsigned*>(base + 64); }
   __device__ unsigned* done() const { return reinterpret_cast<unsigned*>(base + 128); }
-  __device__ unsigned* picked() const { return reinterpret_cast<unsigned*>(base + 160); }   // actions out so far
-  __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }   // B, nid0, leaf, net, kind
+  // B, nid0 (conv: the parent), leaf, net, kind (0 batch, 1 conv of src, 2 conv of a rebuilt latent), action
+  __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }
   __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
-  __device__ int* acts() const { return reinterpret_cast<int*>(base + 256); }
-  __device__ double* bv(int A) const { return reinterpret_cast<double*>(base + 256 + (A * 4 + 255) / 256 * 256); }
+  // the actions, tagged: batch number << 32 | action (an entry is valid for
+  // the batch whose number it carries: no separate progress counter)
+  __device__ unsigned long long* acts() const { return reinterpret_cast<unsigned long long*>(base + 256); }
+  __device__ double* bv(int A) const { return reinterpret_cast<double*>(base + 256 + (A * 8 + 255) / 256 * 256); }
   // the root's valid mask (child_priors reads it)
   __device__ uint8_t* valid(int A) const {
-    return base + 256 + (A * 4 + 255) / 256 * 256 + (A * 8 + 255) / 256 * 256;
+    return base + 256 + 2 * ((A * 8 + 255) / 256 * 256);
   }
 };
 template <class G>
@@ -477,21 +479,12 @@ __device__ __forceinline__ void job_wait(const JobView& J, int mine, int total) 
 // claim the next unit of batch bseq (of total): -1 when none is left.  Thread 0
 // claims, the workgroup gets it through LDS.  All threads.
 template <class G>
-__device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned bseq, int total, int step,
-                                         bool gated = false) {
+__device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned bseq, int total, int step) {
   if (threadIdx.x == 0) {
     int c0 = -1;
     unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {                                       // (a failed CAS means another claim succeeded)
       if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFFFFFu) >= total) break;
-      if (gated) {                                   // the round's actions must be out (J.picked)
-        const unsigned need = (unsigned)min((int)(c & 0xFFFFFFFFu) + step, total);
-        if (__hip_atomic_load(J.picked(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-          __builtin_amdgcn_s_sleep(2);
-          c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          continue;
-        }
-      }
       if (__hip_atomic_compare_exchange_strong(J.claim(), &c, c + step, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
         c0 = (int)(c & 0xFFFFFFFFu);
@@ -507,16 +500,19 @@ __device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned
 }
 
 // The dynamics conv of a parent as a job (19x19: 5 row strips, each strip
-// independent given the input): src (the rebuilt latent, [C][CS]) -> dst
-// (its Y, [CELLS][C]); strips claimed one at a time.  Returns this
-// workgroup's strips.  All threads.
+// independent given the input): its input -- src ([C][CS], the root's
+// latent) or, with ypar, the latent rebuilt from the parent's Y and E[a]
+// (wino_input_rebuilt: no materialized copy) -- -> dst (its Y, [CELLS][C]);
+// strips claimed one at a time.  Returns this workgroup's strips.  All threads.
 template <class G>
 __device__ __forceinline__ int conv_strips(Smem<G>& sm, const NetParams& np, const JobView& J, unsigned bseq,
-                                           const float* src, float* dst) {
+                                           const float* src, float* dst, const float* ypar = nullptr,
+                                           const float* ea = nullptr) {
   int mine = 0;
   if constexpr (G::WINO) {
     for (int s; (s = job_claim(sm, J, bseq, Wino<G>::NSTRIP, 1)) >= 0; ++mine) {
-      wino_input<G, G::C>(sm.u.v, sm.raw, src, G::CS, nullptr, s);
+      if (ypar) wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s);
+      else wino_input<G, G::C>(sm.u.v, sm.raw, src, G::CS, nullptr, s);
       wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
                                          dst, G::CS, G::CS, nullptr, s);
     }
@@ -525,21 +521,28 @@ __device__ __forceinline__ int conv_strips(Smem<G>& sm, const NetParams& np, con
   return mine;
 }
 
-// The game's workgroup: the parent's conv over the job machinery (src and
-// dst in HBM; dst = the pool slot of node `leaf`).  All threads; returns
+// The game's workgroup: the conv of node `leaf` over the job machinery
+// (dst = its pool slot).  Input: src (HBM, par < 0) or the latent rebuilt
+// from parent par's Y and action act's E rows.  All threads; returns
 // synchronised with dst complete and acquired.
 template <class G>
 __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, const EngineArrays& E, int g,
-                                            int leaf, int net, const float* src, float* dst) {
+                                            int leaf, int net, const float* src, float* dst,
+                                            Stamp* st = nullptr, int par = -1, int act = 0) {
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J);
   if (threadIdx.x == 0) {
     int* info = J.info();
-    info[0] = Wino<G>::NSTRIP; info[1] = 0; info[2] = leaf; info[3] = net; info[4] = 1;
+    info[0] = Wino<G>::NSTRIP; info[1] = par; info[2] = leaf; info[3] = net; info[4] = par >= 0 ? 2 : 1;
+    info[5] = act;
   }
-  job_publish(J, bseq);                              // (the rebuilt latent src reaches the helpers)
-  const int mine = conv_strips<G>(sm, np, J, bseq, src, dst);
+  job_publish(J, bseq);                              // (src / the parent's Y reach the helpers)
+  if (st) st->lap(52);
+  const float* ypar = par >= 0 ? pool_of<G>(E, g) + (size_t)par * G::C * G::CS : nullptr;
+  const int mine = conv_strips<G>(sm, np, J, bseq, src, dst, ypar, np.etab + (size_t)act * 9 * G::C);
+  if (st) st->lap(53);
   job_wait(J, mine, Wino<G>::NSTRIP);
+  if (st) st->lap(54);
 }
 
 // One child of a batch by ONE wave (batch_expand's per-child work): E[a]
@@ -548,7 +551,9 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
 template <class G, bool LAZY>
 __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                                const TreeView& TV, const float* yg, const ExpandPlan<G>& plan,
-                                               int a, int nid) {
+                                               int a, int nid, Stamp* st = nullptr) {
+  // (st: wave 0's phase cycles in slots 64-66, 68)
+  unsigned long long t0 = st ? st->now() : 0, t1;
   auto& L = sm.u.f;
   typedef decltype(sm.u.f) XL;
   const int lane = lane_id_local();
@@ -558,13 +563,16 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
   const f32x4* e4 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a * 9 * G::C);
   for (int i = lane; i < E4N; i += 64) ewl[i] = e4[i];
   wave_lds_sync();
+  if (st && wave_id() == 0) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
   float rsum, vsum;
   if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
   else expand_wave<G, XL::PROW>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
   wave_lds_sync();
+  if (st && wave_id() == 0) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
   float r, v, x[G::AP];
   heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
   policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
+  if (st && wave_id() == 0) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
   if constexpr (LAZY) {
     float* prow = TV.prior + (size_t)nid * G::A;
 #pragma unroll
@@ -577,6 +585,7 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
     child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
   }
   wave_lds_sync();                     // W.ew / W.xw reused by the wave's next child
+  if (st && wave_id() == 0) { st->wave_add(68, st->now() - t0); }
   return (double)r + sp.discount * (double)v;
 }
 
@@ -586,7 +595,7 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
 template <class G, bool LAZY>
 __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                           const TreeView& TV, const float* yg, const JobView& J, unsigned bseq,
-                                          int B, int nid0, bool helper = false) {
+                                          int B, int nid0, bool helper = false, Stamp* st = nullptr) {
   auto& L = sm.u.f;
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   ExpandPlan<G> plan;
@@ -594,13 +603,22 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
   double* bvg = J.bv(G::A);
   int mine = 0;
   for (;;) {
-    const int c0 = job_claim(sm, J, bseq, B, G::WAVES, helper);
+    const int c0 = job_claim(sm, J, bseq, B, G::WAVES);
     if (c0 < 0) break;
     const int k = c0 + wave;
     if (k < B) {
-      const int a = __builtin_amdgcn_readfirstlane(
-          helper ? __hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : L.acts[k]);
-      const double bv = expand_child<G, LAZY>(sm, np, sp, TV, yg, plan, a, nid0 + k);
+      int a;
+      if (helper) {                                  // (a helper may claim before the game's wave 0 picked it)
+        unsigned long long t = __hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((unsigned)(t >> 32) != bseq) {
+          __builtin_amdgcn_s_sleep(2);
+          t = __hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        a = __builtin_amdgcn_readfirstlane((int)(unsigned)t);
+      } else {
+        a = __builtin_amdgcn_readfirstlane(L.acts[k]);
+      }
+      const double bv = expand_child<G, LAZY>(sm, np, sp, TV, yg, plan, a, nid0 + k, st);
       if (lane_id_local() == 0) bvg[k] = bv;
     }
     mine += (B - c0 < G::WAVES ? B - c0 : G::WAVES);
@@ -621,25 +639,30 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J);
   // the job first (geometry, the root's mask, the actions known already:
-  // i0 of them), then the picks: wave 0 streams the actions out in chunks
-  // (J.picked) while the helpers start on the first rounds
+  // i0 of them), then the picks (pick_all, wave 0; tagged entries: a helper
+  // that claims a round before they are out waits for its entry)
   for (int a = threadIdx.x; a < G::A; a += G::THREADS) J.valid(G::A)[a] = sm.t.valid[a];
   if (threadIdx.x == 0) {
     int* info = J.info();
     info[0] = B; info[1] = nid0; info[2] = leaf; info[3] = net; info[4] = 0;
     *J.pass_prior() = sm.t.pass_prior;
-    for (int k = 0; k < i0; ++k) __hip_atomic_store(J.acts() + k, L.acts[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(J.picked(), (unsigned)i0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < i0; ++k)
+      __hip_atomic_store(J.acts() + k, (unsigned long long)bseq << 32 | (unsigned)L.acts[k], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
   job_publish(J, bseq);
+  if (st) st->lap(40);
   if (wave_id() == 0)
-    pick_sequence<G>(m, n, i0, B - i0, key, sim0, L.acts, nullptr, 12, st, J.acts(), J.picked());
+    pick_all<G>(m, n, i0, B - i0, key, sim0, L.acts, st, J.acts(), bseq);
   __syncthreads();                                   // every pick made (in LDS too)
-  const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0);
+  if (st) st->lap(41);
+  const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0, false, st);
+  if (st) st->lap(42);
   job_wait(J, mine, B);
   const double* bvg = J.bv(G::A);
   for (int k = threadIdx.x; k < B; k += G::THREADS) L.bv[k] = bvg[k];
   __syncthreads();
+  if (st) st->lap(43);
 }
 
 // A helper workgroup of game g (k_selfplay_move's blocks past the games):
@@ -670,9 +693,12 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     const int* info = J.info();
     const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3], kind = info[4];
     const NetParams np = select_params(net != 0, np_b, np_a);
-    if (kind == 1) {                                   // a parent's conv
+    if (kind != 0) {                                   // a parent's conv
+      const int par = info[1], act = info[5];
       const int mine = conv_strips<G>(sm, np, J, s, pool + (size_t)(E.S + 1) * G::C * G::CS,
-                                      pool + (size_t)leaf * G::C * G::CS);
+                                      pool + (size_t)leaf * G::C * G::CS,
+                                      kind == 2 ? pool + (size_t)par * G::C * G::CS : nullptr,
+                                      np.etab + (size_t)act * 9 * G::C);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0 && mine > 0) {
@@ -1201,14 +1227,17 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       float* yleaf = pool + (size_t)leaf * node_floats;
       int yc = sm.t.ycache;
       if (!sm.t.yready) {
-        if (leaf != 0) {
+        const bool sj = shared_jobs<G>(sp);
+        if (leaf != 0 && !sj) {
           const int par = T.path(depth - 1);
           materialize<G>(scratch, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
                          sm.ulds());
         }
         st.lap(81);
-        if (shared_jobs<G>(sp)) {
-          conv_shared<G>(sm, np, E, g, leaf, sp.net, scratch, yleaf);
+        if (sj) {
+          // (the strips read the parent's Y and E rows themselves)
+          conv_shared<G>(sm, np, E, g, leaf, sp.net, scratch, yleaf, &st, leaf != 0 ? T.path(depth - 1) : -1,
+                         leaf != 0 ? nact[leaf] : 0);
         } else {
           latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS,
                                               G::CS, nullptr, &st);

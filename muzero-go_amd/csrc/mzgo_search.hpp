@@ -619,38 +619,107 @@ struct PickSeq {
 
 };
 
-// gout / gprogress (HBM, optional): every published chunk of actions is also
-// stored write-through to gout (agent-scope relaxed stores, drained) and then
-// its count to *gprogress, for other workgroups (batch_expand_shared).
+// gout (HBM, optional): every action also goes to gout[i0 + i] as gtag << 32
+// | action (an agent-scope relaxed store, never waited for), for other
+// workgroups (batch_expand_shared: the tag tells them the entry is current).
 template <class G>
 __device__ __forceinline__ void pick_sequence(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
                                               int sim0, int* out, int* progress = nullptr, int head = 1,
-                                              Stamp* st = nullptr, int* gout = nullptr,
-                                              unsigned* gprogress = nullptr) {
+                                              Stamp* st = nullptr, unsigned long long* gout = nullptr,
+                                              unsigned gtag = 0) {
   const int lane = lane_id_local();
   const unsigned long long t0 = st ? st->now() : 0;
   PickSeq<G> ps(m, n, count, key, sim0);
   const unsigned long long t1 = st ? st->now() : 0;
   if (st) st->wave_add(66, t1 - t0);
-  int next_pub = head < count ? head : count, gdone = 0;
+  int next_pub = head < count ? head : count;
   for (int i = 0; i < count; ++i) {
     const int a = ps.pick(i);
-    if (lane == 0) out[i0 + i] = a;
-    if ((progress || gout) && i + 1 == next_pub) {
+    if (lane == 0) {
+      out[i0 + i] = a;
+      if (gout)
+        __hip_atomic_store(gout + i0 + i, (unsigned long long)gtag << 32 | (unsigned)a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (progress && i + 1 == next_pub) {
       wave_lds_sync();
-      if (progress && lane == 0)
-        __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (gout) {
-        for (int k = gdone + lane; k <= i; k += 64)
-          __hip_atomic_store(gout + i0 + k, out[i0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(gprogress, (unsigned)(i0 + i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gdone = i + 1;
-      }
+      if (lane == 0) __hip_atomic_store(progress, i0 + i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       next_pub = next_pub + 12 < count ? next_pub + 12 : count;
     }
   }
   if (st) st->wave_add(67, st->now() - t1);
+}
+
+// pick_sequence's choices, all at once.  Pick i takes the element of rank r_i
+// among the n - i still remaining; in ranks of the original n elements that
+// is p_i = r_i lifted past every earlier pick: with q_i = r_i to start, for i
+// = count-2 down to 0, q_j += (q_j >= r_i) for every j > i leaves q_j = p_j
+// (step i maps ranks in the set without p_0..p_i to ranks in the set without
+// p_0..p_(i-1); r_i itself is p_i in those coordinates, and no step touches
+// q_i before step i -- the Lehmer code decoded backwards).  Lane j owns q_j:
+// count steps of a compare-and-add instead of count dependent scalar
+// searches.  p -> action through an LDS rank table built in out[i0 ..] (n <=
+// A - i0 entries), read back before the actions overwrite it.
+template <class G, int NG>
+__device__ __forceinline__ void lehmer_lift(uint32_t (&v)[G::AP], const uint32_t (&r)[G::AP], int count) {
+  const int lane = lane_id_local();
+#pragma unroll
+  for (int gi = NG - 1; gi >= 0; --gi) {
+    const int top = min(count - 2, 64 * gi + 63);
+    for (int i = top; i >= 64 * gi; --i) {
+      const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)r[gi], i - 64 * gi);
+      v[gi] += (lane > i - 64 * gi && v[gi] >= s) ? 1u : 0u;
+#pragma unroll
+      for (int q = gi + 1; q < NG; ++q) v[q] += v[q] >= s ? 1u : 0u;
+    }
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void pick_all(const uint64_t (&m)[G::AP], int n, int i0, int count, uint64_t key,
+                                         int sim0, int* out, Stamp* st = nullptr,
+                                         unsigned long long* gout = nullptr, unsigned gtag = 0) {
+  if (count <= 0) return;
+  const int lane = lane_id_local();
+  const unsigned long long t0 = st ? st->now() : 0;
+  PickSeq<G> ps(m, n, count, key, sim0);
+  uint32_t v[G::AP];
+#pragma unroll
+  for (int q = 0; q < G::AP; ++q) v[q] = ps.r[q];
+  const int ng = (count + 63) >> 6;
+  switch (ng) {                                     // (only the groups holding picks)
+#define MZGO_LIFT(K) case K: if constexpr (K <= G::AP) lehmer_lift<G, K>(v, ps.r, count); break;
+    MZGO_LIFT(1) MZGO_LIFT(2) MZGO_LIFT(3) MZGO_LIFT(4) MZGO_LIFT(5) MZGO_LIFT(6)
+#undef MZGO_LIFT
+    default: break;
+  }
+  static_assert(G::AP <= 6, "lehmer_lift dispatch covers up to 6 lane groups");
+  // rank table: the k-th remaining element (ascending) at tab[k]
+  int* tab = out + i0;
+  uint32_t pre = 0;
+#pragma unroll
+  for (int w = 0; w < G::AP; ++w) {
+    const uint32_t lo = (uint32_t)ps.rem[w], hi = (uint32_t)(ps.rem[w] >> 32);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+    if ((ps.rem[w] >> lane) & 1ull) tab[pre + below] = 64 * w + lane;
+    pre += (uint32_t)__builtin_popcountll(ps.rem[w]);
+  }
+  wave_lds_sync();
+  int a[G::AP];
+#pragma unroll
+  for (int q = 0; q < G::AP; ++q) a[q] = (lane + 64 * q < count) ? tab[v[q]] : 0;
+  wave_lds_sync();
+#pragma unroll
+  for (int q = 0; q < G::AP; ++q) {
+    const int j = lane + 64 * q;
+    if (j < count) {
+      out[i0 + j] = a[q];
+      if (gout)
+        __hip_atomic_store(gout + i0 + j, (unsigned long long)gtag << 32 | (unsigned)a[q], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (st) st->wave_add(67, st->now() - t0);
 }
 
 // PUCT over the eligible, all expanded children elig (self_play.py:290-308;

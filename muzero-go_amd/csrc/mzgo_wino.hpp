@@ -306,6 +306,75 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
   }
 }
 
+// wino_input of a REBUILT latent relu(Y + E[a]) (materialize, mzgo_expand.hpp:
+// the dynamics input of a node rebuilt from its parent's conv output Y,
+// self_play.py:87-90) without the channel-major copy: the strip's rows are
+// read straight from Y ([CELLS][C], cell-major, global) in slabs of 4 WAVES
+// channels.  Slab k = channels 4Wk .. 4Wk + 4W-1 = quads Wk .. Wk + W-1 (quad
+// = (h*S4 + s4)*4 + kq, channel 16*(h*S4 + s4) + 4e + kq), one quad per wave
+// (19x19: 12 waves, 2 slabs of 48 channels).  The workgroup loads the slab's
+// cells (W float4 per cell, contiguous), adds E's
+// region row, applies the ReLU and scatters a float4's 4 channels (kq = 0..3)
+// to 4 waves' planes; after a barrier each wave transforms its quad.  The
+// next slab's loads are in flight during the transform.  Values are
+// bit-identical to materialize + wino_input (the same f32 add and select).
+template <class G, int CIN>
+__device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float* __restrict__ raw,
+                                                   const float* __restrict__ ypar, const float* __restrict__ ea,
+                                                   int strip) {
+  typedef Wino<G> W;
+  typedef WinoRaw<G> R;
+  constexpr int RS = R::STRIDE, PW = R::PW, PH = R::PH, C4 = CIN / 4;
+  constexpr int F4 = G::WAVES;                          // float4 per cell per slab
+  static_assert(CIN == G::C && G::WAVES % 4 == 0 && CIN % (4 * F4) == 0, "whole slabs, one quad per wave");
+  constexpr int SLABS = CIN / (4 * F4);
+  constexpr int NI = PH * G::N * F4;                    // float4 per slab
+  constexpr int R4 = (NI + G::THREADS - 1) / G::THREADS;
+  const int lane = lane_id_local();
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+  const int t = lane & 15, e = lane >> 4;
+  const int tt = t < W::T ? t : W::T - 1;
+  const int ty = tt / W::TX, tx = tt - ty * W::TX;
+  const int row0 = strip * W::SROWS - 1;
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(ypar);
+  const f32x4* E4 = reinterpret_cast<const f32x4*>(ea);
+  f32x4 yv[R4], ev[R4];
+  auto load = [&](int k) {
+#pragma unroll
+    for (int r = 0; r < R4; ++r) {
+      const int i = min((int)threadIdx.x + r * G::THREADS, NI - 1);
+      const int cl = i / F4, q4 = i - cl * F4, py = cl / G::N, x = cl - py * G::N, y = row0 + py;
+      const bool on = y >= 0 && y < G::N;
+      const int ry = y <= 0 ? 0 : (y >= G::N - 1 ? 2 : 1), rx = x == 0 ? 0 : (x == G::N - 1 ? 2 : 1);
+      yv[r] = Y4[(on ? y * G::N + x : 0) * C4 + F4 * k + q4];
+      ev[r] = E4[(ry * 3 + rx) * C4 + F4 * k + q4];
+    }
+  };
+  __syncthreads();                                      // the previous conv's epilogue is done with LDS
+  load(0);
+#pragma unroll 1
+  for (int k = 0; k < SLABS; ++k) {
+#pragma unroll
+    for (int r = 0; r < R4; ++r) {
+      const int i = threadIdx.x + r * G::THREADS;
+      if (i < NI) {
+        const int cl = i / F4, q4 = i - cl * F4, py = cl / G::N, x = cl - py * G::N, y = row0 + py;
+        const bool on = y >= 0 && y < G::N;
+        float* dst = raw + ((q4 >> 2) * 4) * 4 * RS + (q4 & 3) * RS + py * PW + x + 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = yv[r][j] + ev[r][j];
+          dst[j * 4 * RS] = on ? (v > 0.f ? v : 0.f) : 0.f;
+        }
+      }
+    }
+    if (k + 1 < SLABS) load(k + 1);
+    __syncthreads();
+    wino_transform_quad<G, CIN>(V, raw + wave * 4 * RS, F4 * k + wave, t, e, ty, tx);
+    __syncthreads();                                    // planes read before the next slab / V before the GEMM
+  }
+}
+
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
 __device__ __forceinline__ constexpr float wino_at2(int oy, int i) {
   return oy == 0 ? (i < 3 ? 1.f : 0.f) : (i == 0 ? 0.f : (i == 2 ? -1.f : 1.f));

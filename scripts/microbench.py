@@ -53,7 +53,8 @@ def main():
     print(json.dumps({"N": N, "G": G, "S": S, **out}))
 
 
-if __name__ == "__main__" and not os.environ.get("STAMPS") and not os.environ.get("MOVE_STAMPS"):
+if __name__ == "__main__" and not os.environ.get("STAMPS") and not os.environ.get("MOVE_STAMPS") \
+        and not os.environ.get("GAME_STAMPS"):
     main()
 
 
@@ -205,8 +206,8 @@ def game_stamps_report():
                       "search_slots_mean_top": [(i, round(v)) for i, v in top],
                       "convs_slowest_game": float(f[slow, 59]), "convs_mean_game": float(f[:, 59].mean()),
                       "wall_slots_mean": {i: round(float(f[:, i].mean())) for i in
-                                          (0, 2, 3, 4, 5, 22, 23, 24, 25, 26, 27, 62, 63, 69, 70, 71, 72, 73, 74,
-                                           75, 76, 77, 78, 79, 81, 82)},
+                                          (0, 2, 3, 4, 5, 22, 23, 24, 25, 26, 27, 40, 41, 42, 43, 52, 53, 54, 62, 63, 69, 70,
+                                           71, 72, 73, 74, 75, 76, 77, 78, 79, 81, 82)},
                       "selects_per_game": float(f[:, 92].mean()), "deep_levels_per_game": float(f[:, 91].mean()),
                       "mean_leaf_depth": float(f[:, 95].sum() / max(f[:, 92].sum(), 1)),
                       "batches_per_game": float(f[:, 31].mean()), "batched_sims_per_game": float(f[:, 28].mean()),
