@@ -29,7 +29,13 @@
 #pragma once
 #include "mzgo_common.hpp"
 
+#ifndef MZGO_XUNROLL
+#define MZGO_XUNROLL 2
+#endif
+
 namespace mzgo {
+
+constexpr int kExpandUnroll = MZGO_XUNROLL;   // expand_wave's unroll on boards of more than 16 passes
 
 template <class G>
 struct ExpandShape {
@@ -252,10 +258,7 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   const char* Eb = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew) + j);
   float* xr = xw + PROW + cg;
   // every pass unrolled on small boards; two at a time on 19x19 (46 passes)
-#ifndef MZGO_XUNROLL
-#define MZGO_XUNROLL 2
-#endif
-#pragma unroll (P <= 16 ? P : MZGO_XUNROLL)
+#pragma unroll (P <= 16 ? P : kExpandUnroll)
   for (int p = 0; p < P; ++p) {
     const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + plan.at(p));
     f32x4 y[X::PERL], e[X::PERL];

@@ -173,6 +173,24 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
   }
 }
 
+// The dynamics conv of a node whose latent is rebuilt from its parent's Y
+// and E[a] (Winograd boards): latent_conv with wino_input_rebuilt as the
+// input transform -- no materialized copy of the latent.  All threads;
+// returns synchronised (strip boards) / with the stores issued (one strip).
+template <class G>
+__device__ __forceinline__ void latent_conv_rebuilt(Smem<G>& sm, const NetParams& np, const float* ypar,
+                                                    const float* ea, float* dst, Stamp* st = nullptr) {
+  if constexpr (G::WINO) {
+    for (int s = 0; s < Wino<G>::NSTRIP; ++s) {
+      wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s);
+      if (st) st->lap(1);
+      wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
+                                        dst, G::CS, G::CS, nullptr, s, st);
+    }
+    if constexpr (Wino<G>::NSTRIP > 1) __syncthreads();
+  }
+}
+
 template <class G>
 __device__ __forceinline__ BoardLds<G> board_lds(Smem<G>& sm) {
   BoardLds<G> b;
@@ -1228,7 +1246,9 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       int yc = sm.t.ycache;
       if (!sm.t.yready) {
         const bool sj = shared_jobs<G>(sp);
-        if (leaf != 0 && !sj) {
+        // Winograd boards rebuild the latent inside the conv's input
+        // transform (wino_input_rebuilt); the others materialize it first
+        if (leaf != 0 && !sj && !G::WINO) {
           const int par = T.path(depth - 1);
           materialize<G>(scratch, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
                          sm.ulds());
@@ -1238,6 +1258,9 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           // (the strips read the parent's Y and E rows themselves)
           conv_shared<G>(sm, np, E, g, leaf, sp.net, scratch, yleaf, &st, leaf != 0 ? T.path(depth - 1) : -1,
                          leaf != 0 ? nact[leaf] : 0);
+        } else if (G::WINO && leaf != 0) {
+          latent_conv_rebuilt<G>(sm, np, pool + (size_t)T.path(depth - 1) * node_floats,
+                                 np.etab + (size_t)nact[leaf] * 9 * G::C, yleaf, &st);
         } else {
           latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS,
                                               G::CS, nullptr, &st);
