@@ -29,13 +29,7 @@
 #pragma once
 #include "mzgo_common.hpp"
 
-#ifndef MZGO_XUNROLL
-#define MZGO_XUNROLL 2
-#endif
-
 namespace mzgo {
-
-constexpr int kExpandUnroll = MZGO_XUNROLL;   // expand_wave's unroll on boards of more than 16 passes
 
 template <class G>
 struct ExpandShape {
@@ -66,12 +60,16 @@ struct ExpandLds {
   // tail arrays: bv (A+16 doubles = 2(A+16) floats) and acts (A ints)
   static constexpr int TAIL = 2 * (G::A + 16) + G::A + 64;
   static constexpr bool BATCH = CACHE ? BASE + G::WAVES * PERW + TAIL <= UF
-                                      : 3 * G::CS + 3 * G::C + G::WAVES * PERW_G + TAIL <= UF;
+                                      : 3 * G::CS + 3 * G::C + 8 * ((G::CELLS + 15) / 16) + G::WAVES * PERW_G + TAIL <= UF;
   static constexpr bool GLOBAL_Y = BATCH && !CACHE;
   static constexpr int XW = CACHE ? 3 * G::CS : G::CS;   // a wave's head rows; the policy row at PROW
   static constexpr int PROW = CACHE ? 2 * G::CS : 0;
   alignas(16) float yc[CACHE ? YC : 4];
   alignas(16) float hw[CACHE || BATCH ? 3 * G::C : 4];
+  // (Y streamed from L2) expand_wave's E-row offsets of pass pairs (load_y):
+  // lane group cg, passes 2pp / 2pp+1 -> rpair[pp*8 + cg], two 16-bit halves
+  static constexpr int RPAIRS = 8 * ((G::CELLS + 15) / 16);
+  uint32_t rpair[GLOBAL_Y ? RPAIRS : 1];
   float xh[3 * G::CS];
   struct Wave {
     alignas(16) float xw[XW];             // the child's policy sums per cell (at PROW)
@@ -190,16 +188,29 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
 
 // Per-lane plan of a wave's expansion passes (expand_wave): lane (j, cg)
 // takes cells cg + 8 p in pass p; off packs, per pass, the byte offset of
-// the cell's region row E[a][region] (two 16-bit halves per dword; cells past
-// the board read region 0 and are discarded).  Built once per batch.
+// the cell's region row E[a][region] (two 16-bit halves per dword: passes 2pp
+// and 2pp + 1; cells past the board read region 0 and are discarded).  Built
+// once per batch, in registers -- or, on boards of more than 16 passes
+// (19x19: 46), read per pass pair from the LDS table ExpandLds::rpair.
 template <class G>
 struct ExpandPlan {
   static constexpr int PASSES = (G::CELLS + 7) / 8;
-  static constexpr bool TABLE = PASSES <= 16;         // else (19x19) each pass works its region out
+  static constexpr bool TABLE = PASSES <= 16;
   uint32_t off[TABLE ? (PASSES + 1) / 2 : 1];
+  const uint32_t* tab;
   static_assert(8 * PASSES <= G::CS, "the last pass's cells stay inside the head rows");
   static_assert(8 * 4 * G::C < 65536, "16-bit region offsets");
-  __device__ __forceinline__ void init() {
+  // the packed offsets of one lane group's pass pairs (cells cg + 16 pp, + 8): the table entry
+  __device__ __forceinline__ static uint32_t pair_entry(int pp, int cg) {
+    auto off1 = [](int cell) { return cell < G::CELLS ? (uint32_t)region_of<G>(cell) * (uint32_t)G::C * 4u : 0u; };
+    return off1(cg + 16 * pp) | (off1(cg + 16 * pp + 8) << 16);
+  }
+  __device__ __forceinline__ uint32_t pair(int pp) const {
+    if constexpr (TABLE) return off[pp];
+    else return tab[pp * 8 + (lane_id_local() >> 3)];
+  }
+  __device__ __forceinline__ void init(const uint32_t* t = nullptr) {
+    if constexpr (!TABLE) tab = t;
     if constexpr (TABLE) {
       const int cg = lane_id_local() >> 3;
 #pragma unroll
@@ -210,14 +221,6 @@ struct ExpandPlan {
         const uint32_t reg = cell < G::CELLS ? (uint32_t)region_of<G>(cell) : 0u;
         off[p >> 1] |= (reg * (uint32_t)G::C * 4u) << (16 * (p & 1));
       }
-    }
-  }
-  __device__ __forceinline__ uint32_t at(int p) const {
-    if constexpr (TABLE) {
-      return (off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu;
-    } else {
-      const int cell = (lane_id_local() >> 3) + 8 * p;
-      return cell < G::CELLS ? (uint32_t)region_of<G>(cell) * (uint32_t)G::C * 4u : 0u;
     }
   }
 };
@@ -258,9 +261,9 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   const char* Eb = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew) + j);
   float* xr = xw + PROW + cg;
   // every pass unrolled on small boards; two at a time on 19x19 (46 passes)
-#pragma unroll (P <= 16 ? P : kExpandUnroll)
-  for (int p = 0; p < P; ++p) {
-    const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + plan.at(p));
+  // one pass: cells cg + 8 p, E rows at byte offset eoff of ew
+  auto pass = [&](int p, uint32_t eoff) {
+    const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + eoff);
     f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
     for (int k = 0; k < X::PERL; ++k) {
@@ -286,6 +289,20 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
       }
     }
     xr[8 * p] = sum8(hp2.x + hp2.y);
+  };
+  if constexpr (ExpandPlan<G>::TABLE) {
+    // every pass unrolled, offsets from the plan's registers
+#pragma unroll
+    for (int p = 0; p < P; ++p) pass(p, (plan.off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu);
+  } else {
+    // pass pairs, one LDS table read per pair (19x19: 23 pairs)
+    static_assert(P % 2 == 0, "whole pass pairs");
+#pragma unroll 1
+    for (int pp = 0; pp < P / 2; ++pp) {
+      const uint32_t w2 = plan.pair(pp);
+      pass(2 * pp, w2 & 0xFFFFu);
+      pass(2 * pp + 1, w2 >> 16);
+    }
   }
   f32x2 dr2 = {0.f, 0.f}, dv2 = {0.f, 0.f};
 #pragma unroll

@@ -324,7 +324,7 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
     const int lane = lane_id_local();
     auto& W = L.wv[wave];
     ExpandPlan<G> plan;
-    plan.init();
+    plan.init(L.rpair);
     // E[a] of the wave's next child, loaded into registers while the current
     // child's heads and rows are written (its action is published by then
     // unless the picks are late; the copy then reads E at the top)
@@ -395,8 +395,8 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
 }
 
 // Node n's Y (global, [CELLS][C]) and the head weights into the LDS copies
-// (GLOBAL_Y boards: the head weights only).  All threads; the caller
-// synchronises.
+// (GLOBAL_Y boards: the head weights and expand_wave's region-offset table
+// only).  All threads; the caller synchronises.
 template <class G>
 __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float* head_w) {
   auto& L = sm.u.f;
@@ -408,6 +408,8 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
   }
   if constexpr (XL::CACHE || XL::BATCH)
     for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
+  if constexpr (XL::GLOBAL_Y)
+    for (int i = threadIdx.x; i < XL::RPAIRS; i += G::THREADS) L.rpair[i] = ExpandPlan<G>::pair_entry(i >> 3, i & 7);
 }
 
 // ---------------------------------------------------------------------------
@@ -617,7 +619,7 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
   auto& L = sm.u.f;
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   ExpandPlan<G> plan;
-  plan.init();
+  plan.init(L.rpair);
   double* bvg = J.bv(G::A);
   int mine = 0;
   for (;;) {
