@@ -205,9 +205,9 @@ struct ExpandPlan {
     auto off1 = [](int cell) { return cell < G::CELLS ? (uint32_t)region_of<G>(cell) * (uint32_t)G::C * 4u : 0u; };
     return off1(cg + 16 * pp) | (off1(cg + 16 * pp + 8) << 16);
   }
-  __device__ __forceinline__ uint32_t pair(int pp) const {
+  __device__ __forceinline__ uint32_t pair(int pp, int cg) const {
     if constexpr (TABLE) return off[pp];
-    else return tab[pp * 8 + (lane_id_local() >> 3)];
+    else return tab[pp * 8 + cg];
   }
   __device__ __forceinline__ void init(const uint32_t* t = nullptr) {
     if constexpr (!TABLE) tab = t;
@@ -261,8 +261,9 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   const char* Eb = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew) + j);
   float* xr = xw + PROW + cg;
   // every pass unrolled on small boards; two at a time on 19x19 (46 passes)
-  // one pass: cells cg + 8 p, E rows at byte offset eoff of ew
-  auto pass = [&](int p, uint32_t eoff) {
+  // one pass: cells cg + 8 p, E rows at byte offset eoff of ew (LAST: the
+  // final pass, whose cells past the board stay out of the sums)
+  auto pass = [&](int p, uint32_t eoff, bool last) {
     const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + eoff);
     f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
@@ -274,7 +275,7 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
 #endif
       e[k] = E4[8 * k];
     }
-    const bool live = G::CELLS % 8 == 0 || p < P - 1 || cg + 8 * p < G::CELLS;
+    const bool live = G::CELLS % 8 == 0 || !last || cg + 8 * p < G::CELLS;
     f32x2 hp2 = {0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < X::PERL; ++k) {
@@ -293,16 +294,20 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   if constexpr (ExpandPlan<G>::TABLE) {
     // every pass unrolled, offsets from the plan's registers
 #pragma unroll
-    for (int p = 0; p < P; ++p) pass(p, (plan.off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu);
+    for (int p = 0; p < P; ++p) pass(p, (plan.off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu, p == P - 1);
   } else {
-    // pass pairs, one LDS table read per pair (19x19: 23 pairs)
+    // pass pairs, one LDS table read per pair (19x19: 23 pairs); the last
+    // pair (whose second pass holds the board's last cells) peeled off
     static_assert(P % 2 == 0, "whole pass pairs");
 #pragma unroll 1
-    for (int pp = 0; pp < P / 2; ++pp) {
-      const uint32_t w2 = plan.pair(pp);
-      pass(2 * pp, w2 & 0xFFFFu);
-      pass(2 * pp + 1, w2 >> 16);
+    for (int pp = 0; pp < P / 2 - 1; ++pp) {
+      const uint32_t w2 = plan.pair(pp, cg);
+      pass(2 * pp, w2 & 0xFFFFu, false);
+      pass(2 * pp + 1, w2 >> 16, false);
     }
+    const uint32_t w2 = plan.pair(P / 2 - 1, cg);
+    pass(P - 2, w2 & 0xFFFFu, false);
+    pass(P - 1, w2 >> 16, true);
   }
   f32x2 dr2 = {0.f, 0.f}, dv2 = {0.f, 0.f};
 #pragma unroll
