@@ -430,7 +430,7 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
 // batch fails.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int job_bytes(int A) {
-  return 256 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256;
+  return 512 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256;
 }
 constexpr unsigned kJobExit = 0xFFFFFFFFu;
 struct JobView {
@@ -438,16 +438,19 @@ struct JobView {
   __device__ unsigned long long* claim() const { return reinterpret_cast<unsigned long long*>(base); }
   __device__ unsigned* seq() const { return reinterpret_cast<unsigned*>(base + 64); }
   __device__ unsigned* done() const { return reinterpret_cast<unsigned*>(base + 128); }
-  // B, nid0 (conv: the parent), leaf, net, kind (0 batch, 1 conv of src, 2 conv of a rebuilt latent), action
+  // B, nid0 (conv: the parent), leaf, net, kind (0 batch, 1 conv of src, 2 conv of a rebuilt latent,
+  // 3 replay checks), action (3: the root action), depth, batch size
   __device__ int* info() const { return reinterpret_cast<int*>(base + 192); }
   __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
+  // replay checks: the failing simulations found by every workgroup (bit i)
+  __device__ unsigned long long* failm() const { return reinterpret_cast<unsigned long long*>(base + 256); }
   // the actions, tagged: batch number << 32 | action (an entry is valid for
   // the batch whose number it carries: no separate progress counter)
-  __device__ unsigned long long* acts() const { return reinterpret_cast<unsigned long long*>(base + 256); }
-  __device__ double* bv(int A) const { return reinterpret_cast<double*>(base + 256 + (A * 8 + 255) / 256 * 256); }
+  __device__ unsigned long long* acts() const { return reinterpret_cast<unsigned long long*>(base + 512); }
+  __device__ double* bv(int A) const { return reinterpret_cast<double*>(base + 512 + (A * 8 + 255) / 256 * 256); }
   // the root's valid mask (child_priors reads it)
   __device__ uint8_t* valid(int A) const {
-    return base + 256 + 2 * ((A * 8 + 255) / 256 * 256);
+    return base + 512 + 2 * ((A * 8 + 255) / 256 * 256);
   }
 };
 template <class G>
@@ -685,64 +688,6 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
   if (st) st->lap(43);
 }
 
-// A helper workgroup of game g (k_selfplay_move's blocks past the games):
-// jobs until the game's workgroup posts kJobExit (or none comes for ~seconds).
-template <class G>
-__device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, const NetParams& np_b,
-                                            const SearchParams& sp, const EngineArrays& E, int g) {
-  const JobView J = job_of<G>(E, g);
-  const TreeView TV = TreeViewOf<G>::make(E, g);
-  float* pool = pool_of<G>(E, g);
-  unsigned last = 0;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 26); ++spins) {
-        __builtin_amdgcn_s_sleep(8);
-        s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (s == last || s == 0) s = kJobExit;           // (bounded wait: give up)
-      if (s != kJobExit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sm.bc[2] = (int)s;
-    }
-    __syncthreads();
-    const unsigned s = (unsigned)sm.bc[2];
-    if (s == kJobExit) return;
-    last = s;
-    const int* info = J.info();
-    const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3], kind = info[4];
-    const NetParams np = select_params(net != 0, np_b, np_a);
-    if (kind != 0) {                                   // a parent's conv
-      const int par = info[1], act = info[5];
-      const int mine = conv_strips<G>(sm, np, J, s, pool + (size_t)(E.S + 1) * G::C * G::CS,
-                                      pool + (size_t)leaf * G::C * G::CS,
-                                      kind == 2 ? pool + (size_t)par * G::C * G::CS : nullptr,
-                                      np.etab + (size_t)act * 9 * G::C);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0 && mine > 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      continue;
-    }
-    for (int a = threadIdx.x; a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
-    if (threadIdx.x == 0) sm.t.pass_prior = *J.pass_prior();
-    stage_head_scalars(np.hs, sm.t.hsc);
-    load_y<G>(sm, nullptr, np.head_w);                 // (GLOBAL_Y: the head weights only)
-    __syncthreads();
-    const float* yg = pool + (size_t)leaf * G::C * G::CS;
-    const int mine = job_rounds<G, false>(sm, np, sp, TV, yg, J, s, B, nid0, true);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row and value stores
-    __syncthreads();
-    if (threadIdx.x == 0 && mine > 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // dst[0] = w0, dst[k + 1] = dst[k] + (neg ? -v[k] : v[k]) for k < B: the
 // sequential f64 sums (lane 0), 8 at a time without branches, the next 8
 // loads in flight: v is read up to 15 and dst written up to 7 entries past B
@@ -911,9 +856,225 @@ constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
 constexpr int kVerifyMaxDepth = 1 << 20;
 #endif
 
+// verify_batch's checks of path levels l0 .. l0 + nl - 1 (nl <= DV): phases
+// 1a-2 and the exact fallback; failing simulations are OR-ed into vl.failm
+// (the caller zeroes it once).  with_root: also the root's value sums
+// (vl.wroot) on a spare wave.  ract: the root action on the path.  All
+// threads; returns synchronised.
 template <class G, class Acc>
-__device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, Acc& T,
-                                            int* nact, int leaf, int D, int B, int nid, Stamp* st = nullptr) {
+__device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, const Acc& T,
+                                              const int* nact, int D, int B, int l0, int nl, int ract,
+                                              bool with_root, Stamp* st = nullptr) {
+  constexpr int DV = verify_depth<G>();
+  typedef VerifyLds<G, DV> V;
+  V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
+  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+  const int lane = lane_id_local();
+  const bool alt = sp.variant == 0;
+  const double* bv = sm.u.f.bv;
+  if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
+  // ---- 1a. jobs 0..nl-1: level l0 + k's children (one wave each); jobs
+  // nl..2nl-1: x's sequential value sums for those levels, and in the first
+  // group job 2nl: the root's, on other waves at the same time ----
+  const int njobs = 2 * nl + (with_root ? 1 : 0);
+  for (int job = wave; job < njobs; job += G::WAVES) {
+    if (job == 2 * nl) {                          // the root's value sum after i simulations
+      prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
+      continue;
+    }
+    if (job >= nl) {                              // x_l = p_(l+1), depth l + 1
+      const int k = job - nl, l = l0 + k;
+      prefix_sums<G>(T.ws(T.path(l + 1)), bv, B, alt && ((D - l) & 1), vl.wpre[k]);
+      continue;
+    }
+    const int k = job, l = l0 + k;
+    const int p = T.path(l);
+    const int xa = l == 0 ? ract : nact[T.path(l + 1)];
+    double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
+    int nx = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int a = lane + 64 * j;
+      const bool in = a < G::A;
+      double P, w = 0.0;
+      int n = 0;
+      if (l == 0) {
+        P = in ? T.root_prior(a) : 0.0;
+        if constexpr (Acc::LDS) {
+          if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
+        } else {
+          const int c = in ? T.child(0, a) : -1;
+          if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+        }
+      } else {
+        P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
+        const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
+        if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+      }
+      const bool e = P > 0.0;
+      const uint64_t el = __ballot(e);
+      const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
+      const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
+      vl.cP[k][a] = cp;
+      vl.q[k][a] = q;
+      vl.inv1n[k][a] = 1.0 / (double)(1 + n);
+      vl.n[k][a] = n;
+      if (lane == 0) vl.elig[k][j] = el;
+      if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
+      if (j == (xa >> 6)) {
+        nx = __builtin_amdgcn_readlane(n, xa & 63);
+        cpx = dpp::lane(cp, xa & 63);
+      }
+    }
+    wave_minmax(lo, hi);
+    if (lane == 0) {
+      vl.lo_o[k] = lo;
+      vl.hi_o[k] = hi;
+      vl.x[k] = xa;
+      vl.n0[k] = nx;
+      vl.N0[k] = T.vis(p);
+      vl.cpx[k] = cpx;
+    }
+    if (st) st->lap(75);
+  }
+  __syncthreads();
+  if (st) st->lap(76);
+  // ---- 1b. per level, per simulation i (lane i = lane + 64 j): the level
+  // as simulation i's select finds it, and x's score exactly as puct_pick
+  // forms it; a score that is not finite fails i ----
+  for (int k = wave; k < nl; k += G::WAVES) {
+    const int nx = vl.n0[k], N0 = vl.N0[k];
+    const double lo = vl.lo_o[k], hi = vl.hi_o[k], cpx = vl.cpx[k];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int i = lane + 64 * j;
+      bool bad = false;
+      if (i <= B) {
+        const int n1 = nx + i, Ni = N0 + i;
+        const double qxi = n1 > 0 ? vl.wpre[k][i] / (double)n1 : 0.0;
+        const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
+        const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
+        const double sxi = (hii > loi ? (qxi - loi) / (hii - loi) : qxi) + (cpx * sqi) / (double)(1 + n1);
+        vl.qx[k][i] = qxi;
+        vl.invr[k][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;
+        vl.sq[k][i] = sqi;
+        vl.sx[k][i] = sxi;
+        bad = i >= 1 && i < B && !(sxi > -INFINITY);
+      }
+      const uint64_t bb = __ballot(bad);
+      if (lane == 0 && bb) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)bb);
+    }
+    if (st) st->lap(77);
+  }
+  __syncthreads();
+  if (st) st->lap(72);
+  // ---- 2. every (i, l) check at once, transposed: lanes are simulations
+  // i = lane + 64 j, each wave takes every WAVES-th child a of each level.
+  // Screening: the two divisions of a's score as products with reciprocals
+  // (a few ulp off); a decides (l, i) only if its score is clear of x's by
+  // far more than that, else (l, i) is redone below with puct_pick's exact
+  // operations.  i fails if any eligible a != x beats x (puct_pick's first
+  // maximum: a higher score, or an equal one at a lower action). ----
+  const unsigned long long ts0 = st ? st->now() : 0;
+  for (int k = 0; k < nl; ++k) {
+    const int xa = vl.x[k];
+    const double lo_o = vl.lo_o[k], hi_o = vl.hi_o[k];
+    double loi[G::AP], invr[G::AP], sqi[G::AP], sxi[G::AP], tol[G::AP];
+    bool spread[G::AP];
+    uint64_t beaten[G::AP], close[G::AP];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const int i = lane + 64 * j;
+      const int ii = i <= B ? i : B;
+      const double qxi = vl.qx[k][ii];
+      loi[j] = fmin(lo_o, qxi);
+      spread[j] = fmax(hi_o, qxi) > loi[j];
+      invr[j] = vl.invr[k][ii];
+      sqi[j] = vl.sq[k][ii];
+      sxi[j] = vl.sx[k][ii];
+      tol[j] = 1e-12 * (1.0 + fabs(sxi[j]));
+      beaten[j] = 0;
+      close[j] = 0;
+    }
+    // the wave's children a = wave + WAVES k, one per lane k, loaded in one
+    // round trip; the loop broadcasts them with readlane
+    constexpr int KW = (G::A + G::WAVES - 1) / G::WAVES;
+    static_assert(KW <= 64, "one lane per child of the wave");
+    const int amine = wave + G::WAVES * lane;
+    const bool mine = lane < KW && amine < G::A && amine != xa &&
+                      ((vl.elig[k][(amine < G::A ? amine : 0) >> 6] >> (amine & 63)) & 1ull);
+    const int ac = mine ? amine : 0;
+    const double qa_l = vl.q[k][ac], cpa_l = vl.cP[k][ac], ia_l = vl.inv1n[k][ac];
+    const uint64_t todo = __ballot(mine);
+    for (uint64_t mm = todo; mm; mm &= mm - 1) {
+      const int kk = __builtin_ctzll(mm);
+      const double qa = dpp::lane(qa_l, kk), cpa = dpp::lane(cpa_l, kk), ia = dpp::lane(ia_l, kk);
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        if (64 * j >= B) break;                     // (uniform) no simulation i in this register
+        const double sc = (spread[j] ? (qa - loi[j]) * invr[j] : qa) + (cpa * sqi[j]) * ia;
+        beaten[j] |= __ballot(sc > sxi[j] + tol[j]);
+        close[j] |= __ballot(!(fabs(sc - sxi[j]) > tol[j]));
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j) {
+        if (beaten[j]) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)beaten[j]);
+        if (close[j] & ~beaten[j])
+          atomicOr(reinterpret_cast<unsigned long long*>(&vl.exactm[k][j]), (unsigned long long)(close[j] & ~beaten[j]));
+      }
+    }
+  }
+  if (st) st->wave_add(80, st->now() - ts0);
+  __syncthreads();
+  if (st) st->lap(78);
+  // the open (l, i) checks with puct_pick's exact operations (rare)
+  for (int k = 0; k < nl; ++k) {
+    uint64_t open[G::AP];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      const uint64_t o = vl.exactm[k][j] & ~vl.failm[j];
+      open[j] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t)o);
+    }
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) {
+      for (uint64_t mm = open[j]; mm; mm &= mm - 1, ++c) {
+        if (c % G::WAVES != wave) continue;
+        const int i = 64 * j + __builtin_ctzll(mm);
+        if (i < 1 || i >= B) continue;
+        const int xa = vl.x[k];
+        const int nx = vl.n0[k] + i;
+        const double qx = vl.qx[k][i];
+        const double lo = fmin(vl.lo_o[k], qx), hi = fmax(vl.hi_o[k], qx);
+        const double sq = vl.sq[k][i], sx = vl.sx[k][i];
+        uint64_t beat = 0;
+#pragma unroll
+        for (int jj = 0; jj < G::AP; ++jj) {
+          const int a = lane + 64 * jj;
+          const bool el = (vl.elig[k][jj] >> lane) & 1ull;
+          const bool isx = a == xa;
+          const double q = isx ? qx : vl.q[k][a];
+          const int n = isx ? nx : vl.n[k][a];
+          const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
+          const double sc = qn + (vl.cP[k][a] * sq) / (double)(1 + n);
+          beat |= __ballot(el && !isx && (sc > sx || (sc == sx && a < xa)));
+        }
+        if (beat && lane == 0)
+          atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[i >> 6]), 1ull << (i & 63));
+      }
+    }
+  }
+  __syncthreads();
+  if (st) st->lap(79);
+}
+
+template <class G, class Acc>
+__device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const EngineArrays& E, int g,
+                                            const TreeView& TV, Acc& T, int* nact, int leaf, int D, int B, int nid,
+                                            Stamp* st = nullptr) {
   if constexpr (!decltype(sm.u.f)::BATCH) {
     return 0;                                       // (no speculative batches without the batch LDS)
   } else {
@@ -921,7 +1082,6 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   typedef VerifyLds<G, DV> V;
   static_assert(sizeof(V) <= sizeof(sm.u.f.wv), "verification arrays overlay the batch buffers");
   V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
-  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
   const int lane = lane_id_local();
   const bool alt = sp.variant == 0;
   const double* bv = sm.u.f.bv;
@@ -929,207 +1089,36 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
   // Levels l0 .. l0 + nl - 1 at a time (every (i, l) check is independent of
   // the others; a failing i is recorded in failm whichever group finds it).
-  for (int l0 = 0; l0 < D; l0 += DV) {
-    const int nl = D - l0 < DV ? D - l0 : DV;
-    if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
-    // ---- 1a. jobs 0..nl-1: level l0 + k's children (one wave each); jobs
-    // nl..2nl-1: x's sequential value sums for those levels, and in the first
-    // group job 2nl: the root's, on other waves at the same time ----
-    const int njobs = 2 * nl + (l0 == 0 ? 1 : 0);
-    for (int job = wave; job < njobs; job += G::WAVES) {
-      if (job == 2 * nl) {                          // the root's value sum after i simulations
-        prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
-        continue;
-      }
-      if (job >= nl) {                              // x_l = p_(l+1), depth l + 1
-        const int k = job - nl, l = l0 + k;
-        prefix_sums<G>(T.ws(T.path(l + 1)), bv, B, alt && ((D - l) & 1), vl.wpre[k]);
-        continue;
-      }
-      const int k = job, l = l0 + k;
-      const int p = T.path(l);
-      const int xa = l == 0 ? sm.t.ract : nact[T.path(l + 1)];
-      double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
-      int nx = 0;
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        const int a = lane + 64 * j;
-        const bool in = a < G::A;
-        double P, w = 0.0;
-        int n = 0;
-        if (l == 0) {
-          P = in ? T.root_prior(a) : 0.0;
-          if constexpr (Acc::LDS) {
-            if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
-          } else {
-            const int c = in ? T.child(0, a) : -1;
-            if (c >= 0) { n = T.vis(c); w = T.ws(c); }
-          }
-        } else {
-          P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
-          const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
-          if (c >= 0) { n = T.vis(c); w = T.ws(c); }
-        }
-        const bool e = P > 0.0;
-        const uint64_t el = __ballot(e);
-        const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
-        const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
-        vl.cP[k][a] = cp;
-        vl.q[k][a] = q;
-        vl.inv1n[k][a] = 1.0 / (double)(1 + n);
-        vl.n[k][a] = n;
-        if (lane == 0) vl.elig[k][j] = el;
-        if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
-        if (j == (xa >> 6)) {
-          nx = __builtin_amdgcn_readlane(n, xa & 63);
-          cpx = dpp::lane(cp, xa & 63);
-        }
-      }
-      wave_minmax(lo, hi);
-      if (lane == 0) {
-        vl.lo_o[k] = lo;
-        vl.hi_o[k] = hi;
-        vl.x[k] = xa;
-        vl.n0[k] = nx;
-        vl.N0[k] = T.vis(p);
-        vl.cpx[k] = cpx;
-      }
-      if (st) st->lap(75);
+  // With helper workgroups (HBM trees), several groups are a job: each
+  // workgroup claims groups and ORs its failing simulations into J.failm.
+  const int ngroups = (D + DV - 1) / DV;
+  const bool shared = !Acc::LDS && shared_jobs<G>(sp) && ngroups > 1;
+  if (shared) {
+    const JobView J = job_of<G>(E, g);
+    const unsigned bseq = job_begin(J);
+    if (threadIdx.x == 0) {
+      int* info = J.info();
+      info[0] = ngroups; info[1] = nid; info[2] = leaf; info[3] = 0; info[4] = 3;
+      info[5] = sm.t.ract; info[6] = D; info[7] = B;
     }
+    if (threadIdx.x < G::AP) __hip_atomic_store(J.failm() + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    job_publish(J, bseq);                          // (J.bv holds the batch's values already)
+    int mine = 0;
+    for (int grp; (grp = job_claim(sm, J, bseq, ngroups, 1)) >= 0; ++mine)
+      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, grp * DV, min(DV, D - grp * DV), sm.t.ract, false, st);
+    if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
+      __hip_atomic_fetch_or(J.failm() + threadIdx.x, (unsigned long long)vl.failm[threadIdx.x], __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (st) st->lap(76);
-    // ---- 1b. per level, per simulation i (lane i = lane + 64 j): the level
-    // as simulation i's select finds it, and x's score exactly as puct_pick
-    // forms it; a score that is not finite fails i ----
-    for (int k = wave; k < nl; k += G::WAVES) {
-      const int nx = vl.n0[k], N0 = vl.N0[k];
-      const double lo = vl.lo_o[k], hi = vl.hi_o[k], cpx = vl.cpx[k];
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        const int i = lane + 64 * j;
-        bool bad = false;
-        if (i <= B) {
-          const int n1 = nx + i, Ni = N0 + i;
-          const double qxi = n1 > 0 ? vl.wpre[k][i] / (double)n1 : 0.0;
-          const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
-          const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
-          const double sxi = (hii > loi ? (qxi - loi) / (hii - loi) : qxi) + (cpx * sqi) / (double)(1 + n1);
-          vl.qx[k][i] = qxi;
-          vl.invr[k][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;
-          vl.sq[k][i] = sqi;
-          vl.sx[k][i] = sxi;
-          bad = i >= 1 && i < B && !(sxi > -INFINITY);
-        }
-        const uint64_t bb = __ballot(bad);
-        if (lane == 0 && bb) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)bb);
-      }
-      if (st) st->lap(77);
-    }
-    __syncthreads();
-    if (st) st->lap(72);
-    // ---- 2. every (i, l) check at once, transposed: lanes are simulations
-    // i = lane + 64 j, each wave takes every WAVES-th child a of each level.
-    // Screening: the two divisions of a's score as products with reciprocals
-    // (a few ulp off); a decides (l, i) only if its score is clear of x's by
-    // far more than that, else (l, i) is redone below with puct_pick's exact
-    // operations.  i fails if any eligible a != x beats x (puct_pick's first
-    // maximum: a higher score, or an equal one at a lower action). ----
-    const unsigned long long ts0 = st ? st->now() : 0;
-    for (int k = 0; k < nl; ++k) {
-      const int xa = vl.x[k];
-      const double lo_o = vl.lo_o[k], hi_o = vl.hi_o[k];
-      double loi[G::AP], invr[G::AP], sqi[G::AP], sxi[G::AP], tol[G::AP];
-      bool spread[G::AP];
-      uint64_t beaten[G::AP], close[G::AP];
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        const int i = lane + 64 * j;
-        const int ii = i <= B ? i : B;
-        const double qxi = vl.qx[k][ii];
-        loi[j] = fmin(lo_o, qxi);
-        spread[j] = fmax(hi_o, qxi) > loi[j];
-        invr[j] = vl.invr[k][ii];
-        sqi[j] = vl.sq[k][ii];
-        sxi[j] = vl.sx[k][ii];
-        tol[j] = 1e-12 * (1.0 + fabs(sxi[j]));
-        beaten[j] = 0;
-        close[j] = 0;
-      }
-      // the wave's children a = wave + WAVES k, one per lane k, loaded in one
-      // round trip; the loop broadcasts them with readlane
-      constexpr int KW = (G::A + G::WAVES - 1) / G::WAVES;
-      static_assert(KW <= 64, "one lane per child of the wave");
-      const int amine = wave + G::WAVES * lane;
-      const bool mine = lane < KW && amine < G::A && amine != xa &&
-                        ((vl.elig[k][(amine < G::A ? amine : 0) >> 6] >> (amine & 63)) & 1ull);
-      const int ac = mine ? amine : 0;
-      const double qa_l = vl.q[k][ac], cpa_l = vl.cP[k][ac], ia_l = vl.inv1n[k][ac];
-      const uint64_t todo = __ballot(mine);
-      for (uint64_t mm = todo; mm; mm &= mm - 1) {
-        const int kk = __builtin_ctzll(mm);
-        const double qa = dpp::lane(qa_l, kk), cpa = dpp::lane(cpa_l, kk), ia = dpp::lane(ia_l, kk);
-#pragma unroll
-        for (int j = 0; j < G::AP; ++j) {
-          if (64 * j >= B) break;                     // (uniform) no simulation i in this register
-          const double sc = (spread[j] ? (qa - loi[j]) * invr[j] : qa) + (cpa * sqi[j]) * ia;
-          beaten[j] |= __ballot(sc > sxi[j] + tol[j]);
-          close[j] |= __ballot(!(fabs(sc - sxi[j]) > tol[j]));
-        }
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int j = 0; j < G::AP; ++j) {
-          if (beaten[j]) atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[j]), (unsigned long long)beaten[j]);
-          if (close[j] & ~beaten[j])
-            atomicOr(reinterpret_cast<unsigned long long*>(&vl.exactm[k][j]), (unsigned long long)(close[j] & ~beaten[j]));
-        }
-      }
-    }
-    if (st) st->wave_add(80, st->now() - ts0);
-    __syncthreads();
-    if (st) st->lap(78);
-    // the open (l, i) checks with puct_pick's exact operations (rare)
-    for (int k = 0; k < nl; ++k) {
-      uint64_t open[G::AP];
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        const uint64_t o = vl.exactm[k][j] & ~vl.failm[j];
-        open[j] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
-                  __builtin_amdgcn_readfirstlane((uint32_t)o);
-      }
-      int c = 0;
-#pragma unroll
-      for (int j = 0; j < G::AP; ++j) {
-        for (uint64_t mm = open[j]; mm; mm &= mm - 1, ++c) {
-          if (c % G::WAVES != wave) continue;
-          const int i = 64 * j + __builtin_ctzll(mm);
-          if (i < 1 || i >= B) continue;
-          const int xa = vl.x[k];
-          const int nx = vl.n0[k] + i;
-          const double qx = vl.qx[k][i];
-          const double lo = fmin(vl.lo_o[k], qx), hi = fmax(vl.hi_o[k], qx);
-          const double sq = vl.sq[k][i], sx = vl.sx[k][i];
-          uint64_t beat = 0;
-#pragma unroll
-          for (int jj = 0; jj < G::AP; ++jj) {
-            const int a = lane + 64 * jj;
-            const bool el = (vl.elig[k][jj] >> lane) & 1ull;
-            const bool isx = a == xa;
-            const double q = isx ? qx : vl.q[k][a];
-            const int n = isx ? nx : vl.n[k][a];
-            const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
-            const double sc = qn + (vl.cP[k][a] * sq) / (double)(1 + n);
-            beat |= __ballot(el && !isx && (sc > sx || (sc == sx && a < xa)));
-          }
-          if (beat && lane == 0)
-            atomicOr(reinterpret_cast<unsigned long long*>(&vl.failm[i >> 6]), 1ull << (i & 63));
-        }
-      }
-    }
-    __syncthreads();
-    if (st) st->lap(79);
+    job_wait(J, mine, ngroups);
+    if (threadIdx.x < G::AP)
+      vl.failm[threadIdx.x] = __hip_atomic_load(J.failm() + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    for (int l0 = 0; l0 < D; l0 += DV)
+      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, l0, D - l0 < DV ? D - l0 : DV, sm.t.ract, l0 == 0, st);
   }
-  if (D == 0 && threadIdx.x == 0) prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
+  if ((D == 0 || shared) && threadIdx.x == 0) prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
   if (threadIdx.x == 0) {
     int f = B;
 #pragma unroll
@@ -1176,6 +1165,91 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   __syncthreads();
   if (st) st->lap(74);
   return m;
+  }
+}
+
+// A helper workgroup of game g (k_selfplay_move's blocks past the games):
+// jobs until the game's workgroup posts kJobExit (or none comes for ~seconds):
+// batch expansions, parent convs and replay checks.
+template <class G>
+__device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, const NetParams& np_b,
+                                            const SearchParams& sp, const EngineArrays& E, int g) {
+  const JobView J = job_of<G>(E, g);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  float* pool = pool_of<G>(E, g);
+  unsigned last = 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 26); ++spins) {
+        __builtin_amdgcn_s_sleep(8);
+        s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (s == last || s == 0) s = kJobExit;           // (bounded wait: give up)
+      if (s != kJobExit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sm.bc[2] = (int)s;
+    }
+    __syncthreads();
+    const unsigned s = (unsigned)sm.bc[2];
+    if (s == kJobExit) return;
+    last = s;
+    const int* info = J.info();
+    const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3], kind = info[4];
+    const NetParams np = select_params(net != 0, np_b, np_a);
+    if (kind == 3) {                                   // replay checks of a batch (verify_batch)
+      constexpr int DV = verify_depth<G>();
+      typedef VerifyLds<G, DV> V;
+      V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
+      const int ngroups = B, ract = info[5], D = info[6], nb = info[7];
+      const double* bvg = J.bv(G::A);
+      for (int k = threadIdx.x; k < nb; k += G::THREADS) sm.u.f.bv[k] = bvg[k];
+      if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
+      __syncthreads();
+      const TreeAcc<G, false> T(TV, sm.t);
+      const int* nact = E.nact + (size_t)g * ((size_t)E.S + 1);
+      int mine = 0;
+      for (int grp; (grp = job_claim(sm, J, s, ngroups, 1)) >= 0; ++mine)
+        verify_levels<G, TreeAcc<G, false>>(sm, sp, TV, T, nact, D, nb, grp * DV, min(DV, D - grp * DV), ract,
+                                            false);
+      if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
+        __hip_atomic_fetch_or(J.failm() + threadIdx.x, (unsigned long long)vl.failm[threadIdx.x], __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0 && mine > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    if (kind != 0) {                                   // a parent's conv
+      const int par = info[1], act = info[5];
+      const int mine = conv_strips<G>(sm, np, J, s, pool + (size_t)(E.S + 1) * G::C * G::CS,
+                                      pool + (size_t)leaf * G::C * G::CS,
+                                      kind == 2 ? pool + (size_t)par * G::C * G::CS : nullptr,
+                                      np.etab + (size_t)act * 9 * G::C);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0 && mine > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    for (int a = threadIdx.x; a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
+    if (threadIdx.x == 0) sm.t.pass_prior = *J.pass_prior();
+    stage_head_scalars(np.hs, sm.t.hsc);
+    load_y<G>(sm, nullptr, np.head_w);                 // (GLOBAL_Y: the head weights only)
+    __syncthreads();
+    const float* yg = pool + (size_t)leaf * G::C * G::CS;
+    const int mine = job_rounds<G, false>(sm, np, sp, TV, yg, J, s, B, nid0, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row and value stores
+    __syncthreads();
+    if (threadIdx.x == 0 && mine > 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1311,7 +1385,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         __syncthreads();
         st.lap(5);
         if (depth <= kVerifyMaxDepth) {
-          const int m = verify_batch<G, Acc>(sm, sp, TV, T, nact, leaf, depth, B, nid, &st);
+          const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st);
           nodes += m;
           sim += m;
           st.lap(63);
