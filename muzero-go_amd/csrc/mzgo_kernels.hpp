@@ -548,10 +548,16 @@ __device__ __forceinline__ int conv_strips(Smem<G>& sm, const NetParams& np, con
 // (dst = its pool slot).  Input: src (HBM, par < 0) or the latent rebuilt
 // from parent par's Y and action act's E rows.  All threads; returns
 // synchronised with dst complete and acquired.
-template <class G>
+// pre(bseq): work of the game's workgroup between the publish and its
+// first strip claim (the next batch's picks: pick_all, wave 0), while the
+// helpers start on the strips.
+struct NoPre {
+  __device__ void operator()(unsigned) const {}
+};
+template <class G, class Pre = NoPre>
 __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, const EngineArrays& E, int g,
                                             int leaf, int net, const float* src, float* dst,
-                                            Stamp* st = nullptr, int par = -1, int act = 0) {
+                                            Stamp* st = nullptr, int par = -1, int act = 0, Pre pre = Pre{}) {
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J);
   if (threadIdx.x == 0) {
@@ -560,6 +566,7 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
     info[5] = act;
   }
   job_publish(J, bseq);                              // (src / the parent's Y reach the helpers)
+  pre(bseq);
   if (st) st->lap(52);
   const float* ypar = par >= 0 ? pool_of<G>(E, g) + (size_t)par * G::C * G::CS : nullptr;
   const int mine = conv_strips<G>(sm, np, J, bseq, src, dst, ypar, np.etab + (size_t)act * 9 * G::C);
@@ -657,7 +664,7 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
                                                     const EngineArrays& E, int g, const TreeView& TV, int B,
                                                     int nid0, int leaf, int net, const float* yg,
                                                     const uint64_t (&m)[G::AP], int n, int i0, uint64_t key,
-                                                    int sim0, Stamp* st = nullptr) {
+                                                    int sim0, Stamp* st = nullptr, bool prepicked = false) {
   auto& L = sm.u.f;
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J);
@@ -675,12 +682,18 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
   }
   job_publish(J, bseq);
   if (st) st->lap(40);
-  if (wave_id() == 0)
+  // (prepicked: the actions i0.. went out during the parent's conv job,
+  // tagged for this batch; the workgroup reads them from the job like a
+  // helper and copies them back into L.acts, which the conv overwrote)
+  if (!prepicked && wave_id() == 0)
     pick_all<G>(m, n, i0, B - i0, key, sim0, L.acts, st, J.acts(), bseq);
   __syncthreads();                                   // every pick made (in LDS too)
   if (st) st->lap(41);
-  const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0, false, st);
+  const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0, prepicked, st);
   if (st) st->lap(42);
+  if (prepicked)
+    for (int k = threadIdx.x; k < B; k += G::THREADS)
+      L.acts[k] = (int)(unsigned)__hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   job_wait(J, mine, B);
   const double* bvg = J.bv(G::A);
   for (int k = threadIdx.x; k < B; k += G::THREADS) L.bv[k] = bvg[k];
@@ -747,21 +760,6 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     __syncthreads();
     const int K = sm.t.bcast;
     if (K == 0) return 0;
-    // the root's conv Y (its latent is in the scratch slot), then Y and the
-    // head weights into LDS.  The conv overwrites the whole union, so the
-    // batch's LDS buffers are filled only after it.
-    if (shared_jobs<G>(sp)) {
-      conv_shared<G>(sm, np, E, g, 0, sp.net, scratch, pool);
-    } else {
-      latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
-                                          nullptr);
-    }
-    __syncthreads();
-    if (st) st->lap(60);
-    load_y<G>(sm, pool, np.head_w);
-    if (threadIdx.x == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
-    __syncthreads();
-    if (st) st->lap(61);
     // the simulations' choices: sim k takes the r_k-th (ascending) of the
     // n - k eligible root children not taken yet, r_k = randbelow(draw_k, n - k)
     uint64_t el[G::AP];
@@ -775,8 +773,26 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         n += __popcll(el[j]);
       }
     }
+    // the root's conv Y (its latent is in the scratch slot), then Y and the
+    // head weights into LDS.  The conv overwrites the whole union, so the
+    // batch's LDS buffers are filled only after it.  (Shared jobs: the picks
+    // go out while the helpers run the conv's strips.)
     if (shared_jobs<G>(sp)) {
-      batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, K, 1, 0, sp.net, pool, el, n, 0, key, 0);
+      conv_shared<G>(sm, np, E, g, 0, sp.net, scratch, pool, st, -1, 0, [&](unsigned cb) {
+        if (wave_id() == 0) pick_all<G>(el, n, 0, K, key, 0, L.acts, st, job_of<G>(E, g).acts(), cb + 1);
+      });
+    } else {
+      latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
+                                          nullptr);
+    }
+    __syncthreads();
+    if (st) st->lap(60);
+    load_y<G>(sm, pool, np.head_w);
+    if (threadIdx.x == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
+    __syncthreads();
+    if (st) st->lap(61);
+    if (shared_jobs<G>(sp)) {
+      batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, K, 1, 0, sp.net, pool, el, n, 0, key, 0, nullptr, true);
     } else {
       if (wave_id() == 0) pick_sequence<G>(el, n, 0, K, key, 0, L.acts, &sm.t.npick, G::WAVES);
       batch_expand<G, Acc::LDS>(sm, np, sp, TV, K, 1, pool, st);
@@ -1091,21 +1107,24 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   // the others; a failing i is recorded in failm whichever group finds it).
   // With helper workgroups (HBM trees), several groups are a job: each
   // workgroup claims groups and ORs its failing simulations into J.failm.
-  const int ngroups = (D + DV - 1) / DV;
+  // (shared: one level per group while the groups do not outnumber the 4
+  // workgroups, else DV)
+  const int gs = D <= 4 ? 1 : DV;
+  const int ngroups = (D + gs - 1) / gs;
   const bool shared = !Acc::LDS && shared_jobs<G>(sp) && ngroups > 1;
   if (shared) {
     const JobView J = job_of<G>(E, g);
     const unsigned bseq = job_begin(J);
     if (threadIdx.x == 0) {
       int* info = J.info();
-      info[0] = ngroups; info[1] = nid; info[2] = leaf; info[3] = 0; info[4] = 3;
+      info[0] = ngroups; info[1] = nid; info[2] = leaf; info[3] = gs; info[4] = 3;
       info[5] = sm.t.ract; info[6] = D; info[7] = B;
     }
     if (threadIdx.x < G::AP) __hip_atomic_store(J.failm() + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     job_publish(J, bseq);                          // (J.bv holds the batch's values already)
     int mine = 0;
     for (int grp; (grp = job_claim(sm, J, bseq, ngroups, 1)) >= 0; ++mine)
-      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, grp * DV, min(DV, D - grp * DV), sm.t.ract, false, st);
+      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, grp * gs, min(gs, D - grp * gs), sm.t.ract, false, st);
     if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
       __hip_atomic_fetch_or(J.failm() + threadIdx.x, (unsigned long long)vl.failm[threadIdx.x], __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
@@ -1201,7 +1220,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       constexpr int DV = verify_depth<G>();
       typedef VerifyLds<G, DV> V;
       V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
-      const int ngroups = B, ract = info[5], D = info[6], nb = info[7];
+      const int ngroups = B, gs = info[3], ract = info[5], D = info[6], nb = info[7];
       const double* bvg = J.bv(G::A);
       for (int k = threadIdx.x; k < nb; k += G::THREADS) sm.u.f.bv[k] = bvg[k];
       if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
@@ -1210,7 +1229,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       const int* nact = E.nact + (size_t)g * ((size_t)E.S + 1);
       int mine = 0;
       for (int grp; (grp = job_claim(sm, J, s, ngroups, 1)) >= 0; ++mine)
-        verify_levels<G, TreeAcc<G, false>>(sm, sp, TV, T, nact, D, nb, grp * DV, min(DV, D - grp * DV), ract,
+        verify_levels<G, TreeAcc<G, false>>(sm, sp, TV, T, nact, D, nb, grp * gs, min(gs, D - grp * gs), ract,
                                             false);
       if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
         __hip_atomic_fetch_or(J.failm() + threadIdx.x, (unsigned long long)vl.failm[threadIdx.x], __ATOMIC_RELAXED,
@@ -1320,6 +1339,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       // (from its latent, rebuilt from its parent's Y unless it is the root)
       float* yleaf = pool + (size_t)leaf * node_floats;
       int yc = sm.t.ycache;
+      bool prepicked = false;                            // the batch's picks went out during the conv job
       if (!sm.t.yready) {
         const bool sj = shared_jobs<G>(sp);
         // Winograd boards rebuild the latent inside the conv's input
@@ -1331,9 +1351,21 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         }
         st.lap(81);
         if (sj) {
-          // (the strips read the parent's Y and E rows themselves)
+          // (the strips read the parent's Y and E rows themselves; the batch's
+          // picks are made while the helpers start on them)
+          const int nun0 = sm.t.nunexp, B0 = BATCH ? (nun0 < S - sim ? nun0 : S - sim) : 1;
+          prepicked = BATCH && B0 >= 2;
           conv_shared<G>(sm, np, E, g, leaf, sp.net, scratch, yleaf, &st, leaf != 0 ? T.path(depth - 1) : -1,
-                         leaf != 0 ? nact[leaf] : 0);
+                         leaf != 0 ? nact[leaf] : 0, [&](unsigned cb) {
+                           if (prepicked && wave_id() == 0) {
+                             uint64_t um0[G::AP];
+#pragma unroll
+                             for (int j = 0; j < G::AP; ++j)
+                               um0[j] = sm.t.umask[j] & ((a >> 6) == j ? ~(1ull << (a & 63)) : ~0ull);
+                             pick_all<G>(um0, nun0 - 1, 1, B0 - 1, key, sim + 1, sm.u.f.acts, &st,
+                                         job_of<G>(E, g).acts(), cb + 1);
+                           }
+                         });
         } else if (G::WINO && leaf != 0) {
           latent_conv_rebuilt<G>(sm, np, pool + (size_t)T.path(depth - 1) * node_floats,
                                  np.etab + (size_t)nact[leaf] * 9 * G::C, yleaf, &st);
@@ -1373,7 +1405,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
         if (shared_jobs<G>(sp)) {
           batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf, um, nun - 1, 1, key,
-                                           sim + 1, &st);
+                                           sim + 1, &st, prepicked);
           st.lap(71);
         } else {
           if (wave_id() == 0) {
