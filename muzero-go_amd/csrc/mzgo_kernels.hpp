@@ -214,9 +214,17 @@ constexpr bool rep_needs_scratch() {
   else return false;
 }
 
-template <class G, class PlaneFn>
+// conv2 / conv3 of the representation as jobs (run_search's RepJobs on
+// 19x19 with helper workgroups): jobs(k) runs conv k and returns true, or
+// returns false for the workgroup's own latent_conv.
+struct NoRepJobs {
+  __device__ bool operator()(int) const { return false; }
+};
+
+template <class G, class PlaneFn, class Jobs = NoRepJobs>
 __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np, PlaneFn planes, float* lat,
-                                      int lat_stride, float* scr, unsigned long long* ts = nullptr) {
+                                      int lat_stride, float* scr, unsigned long long* ts = nullptr,
+                                      Jobs jobs = Jobs{}) {
   float* mid = rep_needs_scratch<G>() ? scr : lat;
   for (int i = threadIdx.x; i < 6 * G::CELLS; i += G::THREADS) {
     const int c = i / G::CELLS, j = i - c * G::CELLS;
@@ -232,13 +240,15 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
 #ifdef MZGO_STAMPS
   if (ts) ts[0] = __builtin_amdgcn_s_memtime();
 #endif
-  latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, mid, lat_stride, oc, nullptr);
+  if (!jobs(2))
+    latent_conv<G, 64, 64, 0>(sm, np.w_conv2, np.b_conv2, lat, lat_stride, nullptr, mid, lat_stride, oc, nullptr);
   __syncthreads();                                         // conv2's stores before conv3 reads them
 #ifdef MZGO_STAMPS
   if (ts) ts[1] = __builtin_amdgcn_s_memtime();
 #endif
-  latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, mid, lat_stride, nullptr, lat, lat_stride, oc,
-                              np.head_w + G::C);
+  if (!jobs(3))
+    latent_conv<G, 64, G::C, 2>(sm, np.w_conv3, np.b_conv3, mid, lat_stride, nullptr, lat, lat_stride, oc,
+                                np.head_w + G::C);
   if (wave_id() == 0)
     finalize_heads<G, Smem<G>::HEAD_PARTS>(sm.heads(), false, sm.t.hsc, sm.t.logits, &sm.t.reward, &sm.t.value);
   __syncthreads();
@@ -430,7 +440,7 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
 // batch fails.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int job_bytes(int A) {
-  return 512 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256;
+  return 512 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256 + ((A - 1 + 15) / 16 * 16 * 12 + 255) / 256 * 256;
 }
 constexpr unsigned kJobExit = 0xFFFFFFFFu;
 struct JobView {
@@ -451,6 +461,10 @@ struct JobView {
   // the root's valid mask (child_priors reads it)
   __device__ uint8_t* valid(int A) const {
     return base + 512 + 2 * ((A * 8 + 255) / 256 * 256);
+  }
+  // representation conv3: the head sums per cell [3][CS] of every strip
+  __device__ float* hfin(int A) const {
+    return reinterpret_cast<float*>(base + 512 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256);
   }
 };
 template <class G>
@@ -573,6 +587,52 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
   if (st) st->lap(53);
   job_wait(J, mine, Wino<G>::NSTRIP);
   if (st) st->lap(54);
+}
+
+// The representation's conv2 (CIN 64 -> 64) and conv3 (64 -> C, value and
+// policy head sums per cell into hfin) of a 19x19 root as strip jobs (kinds
+// 4, 5): src -> dst, both [CIN][CS] / [COUT][CS] in HBM (factored search:
+// the scratch slot and node 0's slot).  Returns this workgroup's strips.
+template <class G, int CIN, int COUT, int NH>
+__device__ __forceinline__ int rep_strips(Smem<G>& sm, const JobView& J, unsigned bseq, const float* w,
+                                          const float* b, const float* src, float* dst, const float* head_w,
+                                          float* hfin) {
+  int mine = 0;
+  if constexpr (G::WINO) {
+    for (int s; (s = job_claim(sm, J, bseq, Wino<G>::NSTRIP, 1)) >= 0; ++mine) {
+      wino_input<G, CIN>(sm.u.v, sm.raw, src, G::CS, nullptr, s);
+      wino_conv<G, CIN, COUT, NH>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, hfin, w, b, dst, G::CS, G::CS,
+                                  head_w, s);
+    }
+  }
+  __syncthreads();
+  return mine;
+}
+
+// The game's workgroup: representation conv k (2 or 3) over the job
+// machinery; conv3's head sums come back into sm.hfin.  All threads;
+// returns synchronised.
+template <class G>
+__device__ __forceinline__ void rep_shared(Smem<G>& sm, const NetParams& np, const EngineArrays& E, int g, int net,
+                                           int k) {
+  if constexpr (G::WINO && Wino<G>::NSTRIP > 1) {
+  const JobView J = job_of<G>(E, g);
+  float* pool = pool_of<G>(E, g);
+  float* lat = pool + (size_t)(E.S + 1) * G::C * G::CS;
+  const unsigned bseq = job_begin(J);
+  if (threadIdx.x == 0) {
+    int* info = J.info();
+    info[0] = Wino<G>::NSTRIP; info[1] = 0; info[2] = 0; info[3] = net; info[4] = k == 2 ? 4 : 5;
+  }
+  job_publish(J, bseq);                              // (conv k's input reaches the helpers)
+  const int mine = k == 2 ? rep_strips<G, 64, 64, 0>(sm, J, bseq, np.w_conv2, np.b_conv2, lat, pool, nullptr, sm.hfin)
+                          : rep_strips<G, 64, G::C, 2>(sm, J, bseq, np.w_conv3, np.b_conv3, pool, lat,
+                                                       np.head_w + G::C, J.hfin(G::A));
+  job_wait(J, mine, Wino<G>::NSTRIP);
+  if (k == 3)
+    for (int i = threadIdx.x; i < 2 * G::CS; i += G::THREADS) sm.hfin[i] = J.hfin(G::A)[i];
+  __syncthreads();
+  }
 }
 
 // One child of a batch by ONE wave (batch_expand's per-child work): E[a]
@@ -1242,6 +1302,20 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       }
       continue;
     }
+    if (kind == 4 || kind == 5) {                      // the representation's conv2 / conv3
+      float* lat = pool + (size_t)(E.S + 1) * G::C * G::CS;
+      const int mine = kind == 4 ? rep_strips<G, 64, 64, 0>(sm, J, s, np.w_conv2, np.b_conv2, lat, pool, nullptr,
+                                                            sm.hfin)
+                                 : rep_strips<G, 64, G::C, 2>(sm, J, s, np.w_conv3, np.b_conv3, pool, lat,
+                                                              np.head_w + G::C, J.hfin(G::A));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0 && mine > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
     if (kind != 0) {                                   // a parent's conv
       const int par = info[1], act = info[5];
       const int mine = conv_strips<G>(sm, np, J, s, pool + (size_t)(E.S + 1) * G::C * G::CS,
@@ -1531,7 +1605,10 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
   const size_t node_floats = (size_t)G::C * G::CS;
   // root latent: node 0's slot (direct; node 1's slot is strip-conv scratch) or
   // the scratch slot (factored: node 0's slot receives its conv Y)
-  if (sp.factored)
+  if (sp.factored && shared_jobs<G>(sp))
+    representation<G>(sm, np, planes, pool + (size_t)(E.S + 1) * node_floats, G::CS, pool, ts ? ts + 3 : nullptr,
+                      [&](int k) { rep_shared<G>(sm, np, E, g, sp.net, k); return true; });
+  else if (sp.factored)
     representation<G>(sm, np, planes, pool + (size_t)(E.S + 1) * node_floats, G::CS, pool, ts ? ts + 3 : nullptr);
   else
     representation<G>(sm, np, planes, pool, G::CS, pool + node_floats, ts ? ts + 3 : nullptr);
