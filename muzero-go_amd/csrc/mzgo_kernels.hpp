@@ -926,6 +926,9 @@ template <class G>
 constexpr int verify_depth() { return G::AP > 2 ? 2 : 8; }
 // leaves deeper than this replay their batch one select at a time instead
 // (MZGO_VERIFY_MAX_DEPTH to compare the two; the trees are the same)
+#ifndef MZGO_PICK_ALL
+#define MZGO_PICK_ALL 0   // unshared batches: picks one by one, streamed (0) or all at once (1)
+#endif
 #ifdef MZGO_VERIFY_MAX_DEPTH
 constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
 #else
@@ -1483,7 +1486,14 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           st.lap(71);
         } else {
           if (wave_id() == 0) {
+#if MZGO_PICK_ALL
+            // every pick at once (pick_all), then published together
+            pick_all<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &st);
+            wave_lds_sync();
+            if (lane_id() == 0) __hip_atomic_store(&sm.t.npick, B, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
             pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1, &st);
+#endif
             st.lap(71);
           }
           batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
