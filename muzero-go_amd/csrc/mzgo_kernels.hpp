@@ -482,11 +482,11 @@ __device__ __forceinline__ bool shared_jobs(const SearchParams& sp) {
 
 // A job's batch number (unique within a launch: the host zeroes the jobs
 // before it) with the claim word and the done counter reset for it.  Thread 0.
-__device__ __forceinline__ unsigned job_begin(const JobView& J) {
+__device__ __forceinline__ unsigned job_begin(const JobView& J, unsigned first = 0) {
   const unsigned bseq = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   if (threadIdx.x == 0) {
     __hip_atomic_store(J.done(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32 | first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return bseq;
 }
@@ -719,12 +719,16 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
 // The game's workgroup: batch_expand over the job machinery (B children of
 // leaf `leaf` whose Y is yg, actions in L.acts, node ids nid0 + k); L.bv
 // gets every child's backup value.
-template <class G, bool LAZY>
+struct NoWait {
+  __device__ void operator()() const {}
+};
+template <class G, bool LAZY, class Wait = NoWait>
 __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                                     const EngineArrays& E, int g, const TreeView& TV, int B,
                                                     int nid0, int leaf, int net, const float* yg,
                                                     const uint64_t (&m)[G::AP], int n, int i0, uint64_t key,
-                                                    int sim0, Stamp* st = nullptr, bool prepicked = false) {
+                                                    int sim0, Stamp* st = nullptr, bool prepicked = false,
+                                                    Wait pre_wait = Wait{}) {
   auto& L = sm.u.f;
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J);
@@ -754,6 +758,7 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
   if (prepicked)
     for (int k = threadIdx.x; k < B; k += G::THREADS)
       L.acts[k] = (int)(unsigned)__hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  pre_wait();                                        // (the replay checks' first level rows, verify_preload)
   job_wait(J, mine, B);
   const double* bvg = J.bv(G::A);
   for (int k = threadIdx.x; k < B; k += G::THREADS) L.bv[k] = bvg[k];
@@ -935,15 +940,74 @@ constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
 constexpr int kVerifyMaxDepth = 1 << 20;
 #endif
 
+// Phase 1a of verify_batch for one path level l (row k of vl): its
+// children's c_puct * P, q, 1 / (1 + n), n and eligibility, the min / max of
+// q over the eligible children other than x_l, and x_l's terms.  Reads the
+// tree only (not the batch's values), so it may run before the batch is
+// done.  Wave-level.
+template <class G, class Acc, class V>
+__device__ __forceinline__ void verify_load_level(Smem<G>& sm, const SearchParams& sp, const TreeView& TV,
+                                                  const Acc& T, const int* nact, V& vl, int k, int l, int ract) {
+  const int lane = lane_id_local();
+  const int p = T.path(l);
+  const int xa = l == 0 ? ract : nact[T.path(l + 1)];
+  double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
+  int nx = 0;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j) {
+    const int a = lane + 64 * j;
+    const bool in = a < G::A;
+    double P, w = 0.0;
+    int n = 0;
+    if (l == 0) {
+      P = in ? T.root_prior(a) : 0.0;
+      if constexpr (Acc::LDS) {
+        if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
+      } else {
+        const int c = in ? T.child(0, a) : -1;
+        if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+      }
+    } else {
+      P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
+      const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
+      if (c >= 0) { n = T.vis(c); w = T.ws(c); }
+    }
+    const bool e = P > 0.0;
+    const uint64_t el = __ballot(e);
+    const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
+    const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
+    vl.cP[k][a] = cp;
+    vl.q[k][a] = q;
+    vl.inv1n[k][a] = 1.0 / (double)(1 + n);
+    vl.n[k][a] = n;
+    if (lane == 0) vl.elig[k][j] = el;
+    if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
+    if (j == (xa >> 6)) {
+      nx = __builtin_amdgcn_readlane(n, xa & 63);
+      cpx = dpp::lane(cp, xa & 63);
+    }
+  }
+  wave_minmax(lo, hi);
+  if (lane == 0) {
+    vl.lo_o[k] = lo;
+    vl.hi_o[k] = hi;
+    vl.x[k] = xa;
+    vl.n0[k] = nx;
+    vl.N0[k] = T.vis(p);
+    vl.cpx[k] = cpx;
+  }
+}
+
 // verify_batch's checks of path levels l0 .. l0 + nl - 1 (nl <= DV): phases
 // 1a-2 and the exact fallback; failing simulations are OR-ed into vl.failm
 // (the caller zeroes it once).  with_root: also the root's value sums
-// (vl.wroot) on a spare wave.  ract: the root action on the path.  All
-// threads; returns synchronised.
+// (vl.wroot) on a spare wave.  ract: the root action on the path.  loaded:
+// the levels' rows are in vl already (verify_preload).  All threads;
+// returns synchronised.
 template <class G, class Acc>
 __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, const Acc& T,
                                               const int* nact, int D, int B, int l0, int nl, int ract,
-                                              bool with_root, Stamp* st = nullptr) {
+                                              bool with_root, Stamp* st = nullptr, bool loaded = false) {
   constexpr int DV = verify_depth<G>();
   typedef VerifyLds<G, DV> V;
   V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
@@ -966,54 +1030,7 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
       prefix_sums<G>(T.ws(T.path(l + 1)), bv, B, alt && ((D - l) & 1), vl.wpre[k]);
       continue;
     }
-    const int k = job, l = l0 + k;
-    const int p = T.path(l);
-    const int xa = l == 0 ? ract : nact[T.path(l + 1)];
-    double lo = INFINITY, hi = -INFINITY, cpx = 0.0;
-    int nx = 0;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j) {
-      const int a = lane + 64 * j;
-      const bool in = a < G::A;
-      double P, w = 0.0;
-      int n = 0;
-      if (l == 0) {
-        P = in ? T.root_prior(a) : 0.0;
-        if constexpr (Acc::LDS) {
-          if (in) { n = sm.t.rvis[a]; w = sm.t.rws[a]; }     // the root-child mirror
-        } else {
-          const int c = in ? T.child(0, a) : -1;
-          if (c >= 0) { n = T.vis(c); w = T.ws(c); }
-        }
-      } else {
-        P = in ? (double)TV.prior[(size_t)p * G::A + a] : 0.0;
-        const int c = in ? TV.child[(size_t)p * G::A + a] : -1;
-        if (c >= 0) { n = T.vis(c); w = T.ws(c); }
-      }
-      const bool e = P > 0.0;
-      const uint64_t el = __ballot(e);
-      const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
-      const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
-      vl.cP[k][a] = cp;
-      vl.q[k][a] = q;
-      vl.inv1n[k][a] = 1.0 / (double)(1 + n);
-      vl.n[k][a] = n;
-      if (lane == 0) vl.elig[k][j] = el;
-      if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
-      if (j == (xa >> 6)) {
-        nx = __builtin_amdgcn_readlane(n, xa & 63);
-        cpx = dpp::lane(cp, xa & 63);
-      }
-    }
-    wave_minmax(lo, hi);
-    if (lane == 0) {
-      vl.lo_o[k] = lo;
-      vl.hi_o[k] = hi;
-      vl.x[k] = xa;
-      vl.n0[k] = nx;
-      vl.N0[k] = T.vis(p);
-      vl.cpx[k] = cpx;
-    }
+    if (!loaded) verify_load_level<G, Acc>(sm, sp, TV, T, nact, vl, job, l0 + job, ract);
     if (st) st->lap(75);
   }
   __syncthreads();
@@ -1150,10 +1167,46 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
   if (st) st->lap(79);
 }
 
+// How verify_batch splits a depth-D path: groups of gs levels; shared: the
+// groups are a job (HBM trees with helper workgroups): one level per group
+// while the groups do not outnumber the 4 workgroups, else DV; otherwise
+// the game's workgroup checks groups of DV itself.  g0: group 0's levels.
+struct VerifyPlan {
+  int gs, ngroups, g0;
+  bool shared;
+};
+template <class G, class Acc>
+__device__ __forceinline__ VerifyPlan verify_plan(const SearchParams& sp, int D) {
+  constexpr int DV = verify_depth<G>();
+  VerifyPlan v;
+  v.gs = D <= 4 ? 1 : DV;
+  v.ngroups = (D + v.gs - 1) / v.gs;
+  v.shared = !Acc::LDS && shared_jobs<G>(sp) && v.ngroups > 1;
+  if (!v.shared) { v.gs = DV; v.ngroups = (D + DV - 1) / DV; }
+  v.g0 = D < v.gs ? D : v.gs;
+  return v;
+}
+
+// verify_batch's group-0 level rows (phase 1a's tree loads), made while the
+// batch's last children are still being expanded (they read the tree, not
+// the batch's values; vl overlays the batch's wave buffers, which the game's
+// workgroup is done with).  All threads; no barrier.
+template <class G, class Acc>
+__device__ __forceinline__ void verify_preload(Smem<G>& sm, const SearchParams& sp, const TreeView& TV, const Acc& T,
+                                               const int* nact, int D) {
+  if constexpr (decltype(sm.u.f)::BATCH) {
+    typedef VerifyLds<G, verify_depth<G>()> V;
+    V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
+    const VerifyPlan v = verify_plan<G, Acc>(sp, D);
+    for (int k = __builtin_amdgcn_readfirstlane(wave_id()); k < v.g0; k += G::WAVES)
+      verify_load_level<G, Acc>(sm, sp, TV, T, nact, vl, k, k, sm.t.ract);
+  }
+}
+
 template <class G, class Acc>
 __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp, const EngineArrays& E, int g,
                                             const TreeView& TV, Acc& T, int* nact, int leaf, int D, int B, int nid,
-                                            Stamp* st = nullptr) {
+                                            Stamp* st = nullptr, bool preloaded = false) {
   if constexpr (!decltype(sm.u.f)::BATCH) {
     return 0;                                       // (no speculative batches without the batch LDS)
   } else {
@@ -1170,14 +1223,14 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   // the others; a failing i is recorded in failm whichever group finds it).
   // With helper workgroups (HBM trees), several groups are a job: each
   // workgroup claims groups and ORs its failing simulations into J.failm.
-  // (shared: one level per group while the groups do not outnumber the 4
-  // workgroups, else DV)
-  const int gs = D <= 4 ? 1 : DV;
-  const int ngroups = (D + gs - 1) / gs;
-  const bool shared = !Acc::LDS && shared_jobs<G>(sp) && ngroups > 1;
+  // (preloaded: group 0's level rows are in vl already -- the game's
+  // workgroup checks group 0 itself, first)
+  const VerifyPlan vp = verify_plan<G, Acc>(sp, D);
+  const int gs = vp.gs, ngroups = vp.ngroups;
+  const bool shared = vp.shared;
   if (shared) {
     const JobView J = job_of<G>(E, g);
-    const unsigned bseq = job_begin(J);
+    const unsigned bseq = job_begin(J, preloaded ? 1u : 0u);
     if (threadIdx.x == 0) {
       int* info = J.info();
       info[0] = ngroups; info[1] = nid; info[2] = leaf; info[3] = gs; info[4] = 3;
@@ -1186,6 +1239,10 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
     if (threadIdx.x < G::AP) __hip_atomic_store(J.failm() + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     job_publish(J, bseq);                          // (J.bv holds the batch's values already)
     int mine = 0;
+    if (preloaded) {
+      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, 0, vp.g0, sm.t.ract, false, st, true);
+      ++mine;
+    }
     for (int grp; (grp = job_claim(sm, J, bseq, ngroups, 1)) >= 0; ++mine)
       verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, grp * gs, min(gs, D - grp * gs), sm.t.ract, false, st);
     if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
@@ -1198,7 +1255,8 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
       vl.failm[threadIdx.x] = __hip_atomic_load(J.failm() + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     for (int l0 = 0; l0 < D; l0 += DV)
-      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, l0, D - l0 < DV ? D - l0 : DV, sm.t.ract, l0 == 0, st);
+      verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, l0, D - l0 < DV ? D - l0 : DV, sm.t.ract, l0 == 0, st,
+                            preloaded && l0 == 0);
   }
   if ((D == 0 || shared) && threadIdx.x == 0) prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
   if (threadIdx.x == 0) {
@@ -1482,7 +1540,9 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           if ((a >> 6) == j) um[j] &= ~(1ull << (a & 63));
         if (shared_jobs<G>(sp)) {
           batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf, um, nun - 1, 1, key,
-                                           sim + 1, &st, prepicked);
+                                           sim + 1, &st, prepicked, [&]() {
+                                             if (depth <= kVerifyMaxDepth) verify_preload<G, Acc>(sm, sp, TV, T, nact, depth);
+                                           });
           st.lap(71);
         } else {
           if (wave_id() == 0) {
@@ -1501,7 +1561,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         __syncthreads();
         st.lap(5);
         if (depth <= kVerifyMaxDepth) {
-          const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st);
+          const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st, shared_jobs<G>(sp));
           nodes += m;
           sim += m;
           st.lap(63);
