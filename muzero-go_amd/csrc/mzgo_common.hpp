@@ -75,8 +75,9 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // deltas per phase into mzgo_stamps[block][phase].
 // ---------------------------------------------------------------------------
 // 0-7 phases (thread 0), 8-19 per-wave conv loops, 20-31 sub-phases,
-// 32-43 per-wave conv-input work, 44-55 per-wave conv-input barrier wait,
-// 56-63 factored simulation detail (see sim_loop), 64-71 batch_expand detail,
+// 40-43 shared batch jobs (publish, picks, own rounds, wait), 52-54 shared
+// conv jobs (publish + picks, own strips, wait), 56-63 factored simulation
+// detail (see sim_loop), 64-71 batch_expand / expand_child detail,
 // 72-82 verify_batch / parent conv detail, 83-87 self-play move phases,
 // 88-90 representation convs, 91-95 select counts (levels at depth >= 2,
 // selects, sequential-replay batches and their simulations, leaf depth sum)
