@@ -638,7 +638,10 @@ __device__ __forceinline__ void rep_shared(Smem<G>& sm, const NetParams& np, con
 // One child of a batch by ONE wave (batch_expand's per-child work): E[a]
 // into W.ew, expand_wave over Y, the heads, the child's prior row (LAZY: its
 // logits) and child row; returns the backup value r + discount * v (every lane).
-template <class G, bool LAZY>
+// LAZYH (HBM trees, the shared batches): the prior row keeps the logits and
+// the child row gets only the sentinel kRawRow in entry 0; select_leaf turns
+// the row into priors when a select first reaches the node (most never are).
+template <class G, bool LAZY, bool LAZYH = false>
 __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                                const TreeView& TV, const float* yg, const ExpandPlan<G>& plan,
                                                int a, int nid, Stamp* st = nullptr) {
@@ -669,6 +672,12 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
     for (int j = 0; j < G::AP; ++j)
       if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
     if (lane == 0) atomicOr(&sm.t.rawp[nid >> 5], 1u << (nid & 31));
+  } else if constexpr (LAZYH) {
+    float* prow = TV.prior + (size_t)nid * G::A;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
+    if (lane == 0) TV.child[(size_t)nid * G::A] = kRawRow;
   } else {
     int* crow = TV.child + (size_t)nid * G::A;
     for (int i = lane; i < G::A; i += 64) crow[i] = -1;
@@ -682,7 +691,7 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
 // The children of job J (batch bseq, B children, node ids nid0 + k, actions
 // in L.acts) a round of WAVES at a time, claimed by CAS; each child's backup
 // value goes to J.bv (HBM).  Returns this workgroup's count.  All threads.
-template <class G, bool LAZY>
+template <class G, bool LAZY, bool LAZYH = false>
 __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                           const TreeView& TV, const float* yg, const JobView& J, unsigned bseq,
                                           int B, int nid0, bool helper = false, Stamp* st = nullptr) {
@@ -708,7 +717,7 @@ __device__ __forceinline__ int job_rounds(Smem<G>& sm, const NetParams& np, cons
       } else {
         a = __builtin_amdgcn_readfirstlane(L.acts[k]);
       }
-      const double bv = expand_child<G, LAZY>(sm, np, sp, TV, yg, plan, a, nid0 + k, st);
+      const double bv = expand_child<G, LAZY, LAZYH>(sm, np, sp, TV, yg, plan, a, nid0 + k, st);
       if (lane_id_local() == 0) bvg[k] = bv;
     }
     mine += (B - c0 < G::WAVES ? B - c0 : G::WAVES);
@@ -753,7 +762,7 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
     pick_all<G>(m, n, i0, B - i0, key, sim0, L.acts, st, J.acts(), bseq);
   __syncthreads();                                   // every pick made (in LDS too)
   if (st) st->lap(41);
-  const int mine = job_rounds<G, LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0, prepicked, st);
+  const int mine = job_rounds<G, LAZY, !LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0, prepicked, st);
   if (st) st->lap(42);
   if (prepicked)
     for (int k = threadIdx.x; k < B; k += G::THREADS)
@@ -1397,7 +1406,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     load_y<G>(sm, nullptr, np.head_w);                 // (GLOBAL_Y: the head weights only)
     __syncthreads();
     const float* yg = pool + (size_t)leaf * G::C * G::CS;
-    const int mine = job_rounds<G, false>(sm, np, sp, TV, yg, J, s, B, nid0, true);
+    const int mine = job_rounds<G, false, true>(sm, np, sp, TV, yg, J, s, B, nid0, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row and value stores
     __syncthreads();
     if (threadIdx.x == 0 && mine > 0) {

@@ -43,6 +43,10 @@ struct TreeView {
   int* path;          // [S+2]
 };
 
+// child-row entry 0 of a node whose prior row still holds its policy logits
+// (HBM trees: expand_child<LAZYH>; select_leaf settles it)
+constexpr int kRawRow = -2;
+
 // Per-game LDS block used by the tree phases.
 template <class G>
 struct TreeLds {
@@ -852,6 +856,29 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         const int a = lane + 64 * j;
         P[j] = a < G::A ? (double)pr_row[a] : 0.0;
         ch[j] = a < G::A ? T.T.child[(size_t)node * G::A + a] : -1;
+      }
+      if constexpr (!Acc::LDS) {
+        // first arrival at a lazily expanded node (HBM trees): the row holds
+        // logits; turn it into priors in place (settle_priors without the
+        // LDS bit), its child row into -1s
+        if (__builtin_amdgcn_readfirstlane(ch[0]) == kRawRow) {
+          if (t.newest >= 0)                      // t.fbuf / t.dbuf: wave 1's while it forms newp
+            while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
+              __builtin_amdgcn_s_sleep(1);
+          float x[G::AP], q[G::AP];
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) x[j] = (float)P[j];
+          child_prior_regs<G>(t, x, q, sp.variant, t.fbuf, t.dbuf);
+          float* prow = const_cast<float*>(pr_row);
+          int* crow = T.T.child + (size_t)node * G::A;
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            const int a = lane + 64 * j;
+            if (a < G::A) { prow[a] = q[j]; crow[a] = -1; }
+            P[j] = a < G::A ? (double)q[j] : 0.0;
+            ch[j] = -1;
+          }
+        }
       }
     }
     // eligible = valid_mask[a] > 0 and prior > 0 (:255-264); every prior is 0
