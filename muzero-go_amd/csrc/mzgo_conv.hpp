@@ -287,6 +287,21 @@ __device__ __forceinline__ void dma16(const void* g, uint32_t lds_dst) {
       : "memory");
 }
 
+// 4 bytes per lane (LDS destination base + lane*4): an L2 prefetch whose data
+// lands in a dummy LDS area
+__device__ __forceinline__ void dma4(const void* g, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds_dst)
+      : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }

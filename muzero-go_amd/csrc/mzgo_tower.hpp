@@ -68,7 +68,8 @@ struct TConvGeo {
 #else
   static constexpr int ADIST = 2;
 #endif
-  static constexpr int LDS = 2 * PB + 2 * WSLOT + 4 * 64 * 4;
+  // + bias and head weights (1 KiB) + the landing area of L2 touches (256 B)
+  static constexpr int LDS = 2 * PB + 2 * WSLOT + 4 * 64 * 4 + 256;
   static_assert(WPW * NW * 1024 == WSLOT, "whole weight pieces per wave");
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(2 * PB >= G::CELLS * 272 + 9 * 64 * 4, "epilogue staging (+ E rows) must fit the patch buffers");
@@ -237,6 +238,17 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
   for (int i = 0; i < T::MT; ++i)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the epilogue's residual lines (this chunk's 64 channels of each pixel) are
+  // touched into L2 at the start of the last step, one 4-byte LDS-DMA per
+  // line landing in a dummy LDS area (its latency overlaps the step's MFMAs;
+  // no DMA is issued after it, so no step's vmcnt count changes)
+  auto touch_epilogue = [&]() {
+    if (!a.res) return;
+    const char* r = reinterpret_cast<const char*>(a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride +
+                                                  (size_t)cg * G::P * 64);
+    constexpr int L0 = G::W + 1, NL = (G::N - 1) * G::W + G::N;     // pixel lines of the board's cells
+    if (tid < NL) dma4(r + (size_t)(L0 + tid) * 128, lds_addr(lds) + (uint32_t)(T::LDS - 256));
+  };
   STAMP_T(tpro);
 
   for (int cc = 0; cc < CC; ++cc) {
@@ -258,6 +270,7 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
         constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
         issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
       }
+      if (s == nsteps - 1) touch_epilogue();
       // One basic block per step (no per-tile branch: a wave past the last
       // tile multiplies a clamped tile and drops it in the epilogue), as
       // groups g = (tap kx, tile i): each group first issues the A fragments
@@ -420,286 +433,6 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
     g[5] += tend - tloop; g[6] += 1;
   }
 #endif
-}
-
-// ---------------------------------------------------------------------------
-// k_tconv2: the same conv with TWO workgroups per CU (19x19).  One workgroup =
-// (board, 64-cout chunk, half of the board's 16-pixel tiles), 4 waves x 3
-// tiles, 60.7 KB of LDS: the k-loop steps over one kernel row of one
-// 32-channel cin chunk (3 taps x 64 couts x 32 cin = 12 KiB of weights), the
-// patch is the band's padded rows of one 32-channel chunk (64-byte pixel
-// rows).  With two workgroups resident per CU, one's barriers, DMA waits and
-// epilogue overlap the other's MFMAs.  64-byte rows hold 4 pieces of 16 B,
-// piece j of row q at j ^ f(q), f(q) = ((q >> 2) & 1) << 1: 16 consecutive
-// rows read as an MFMA fragment (ds_read_b128 lane groups) hit 16 distinct
-// bank groups.  The HBM layouts are k_tconv's: the DMA gathers each 16-byte
-// piece from its place there (per-lane source addresses).
-// Measured (config 5, 256 sims): 29-30 us per conv against k_tconv's 27.4 --
-// the two workgroups of a CU run in phase (a start stagger did not help) and
-// move 1.7x the DMA bytes (both bands load the weights; the patches' halo
-// rows), so it is opt-in (MZGO_TCONV_V2=1); parity-tested like k_tconv.
-// ---------------------------------------------------------------------------
-template <int N>
-struct TConv2Geo {
-  typedef TGeo<N> G;
-  static constexpr int NW = 4, MT = 3;                       // waves, tiles per wave
-  static constexpr int BT = NW * MT;                         // tiles per band
-  static constexpr int BCELLS = BT * 16;                     // cells per band (the last band: fewer)
-  static constexpr int BANDS = (G::TT + BT - 1) / BT;
-  static_assert(BANDS == 2, "two bands per board");
-  // padded input rows of a band: output rows y0..y1 read y0..y1+2
-  static constexpr int rows_of(int band) {
-    const int c0 = band * BCELLS, c1 = (c0 + BCELLS < G::CELLS ? c0 + BCELLS : G::CELLS) - 1;
-    return c1 / N - c0 / N + 3;
-  }
-  static constexpr int PROWS = rows_of(0) > rows_of(1) ? rows_of(0) : rows_of(1);
-  static constexpr int PBYTES = PROWS * G::W * 64;           // one band's patch of one 32-channel chunk
-  static constexpr int PB = (PBYTES + 1023) / 1024 * 1024;
-  static constexpr int PPIECES = PB / 1024;
-  static constexpr int NPW = (PPIECES + NW - 1) / NW;
-  static constexpr int WSLOT = 3 * 64 * 32 * 2;              // one step's weights
-  static constexpr int WPW = WSLOT / 1024 / NW;
-  static constexpr int LDS = 2 * PB + 2 * WSLOT + 4 * 64 * 4;
-  static_assert(WPW * NW * 1024 == WSLOT, "whole weight pieces per wave");
-  static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
-  static_assert(2 * PB + 2 * WSLOT >= BCELLS * 272 + 9 * 64 * 4, "epilogue staging (+ E rows) fits");
-  // next chunk's patch pieces a wave issues at step ky (0, 1) when the band's
-  // patch has `pieces` 1-KiB pieces (pieces past it are not issued)
-  __device__ static int pieces_at(int ky, int wave, int pieces) {
-    const int k0 = ky == 0 ? 0 : (NPW + 1) / 2, k1 = ky == 0 ? (NPW + 1) / 2 : NPW;
-    int n = 0;
-    for (int k = k0; k < k1; ++k) n += (k * NW + wave < pieces) ? 1 : 0;
-    return n;
-  }
-};
-__device__ __forceinline__ int f64row(int q) { return ((q >> 2) & 1) << 1; }
-
-template <int N>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_tconv2(TConvArgs a) {
-  typedef TGeo<N> G;
-  typedef TConv2Geo<N> T;
-  constexpr int NW = T::NW;
-  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
-  const int CO = a.co_chunks, CC = 2 * a.ci_chunks;          // 32-channel cin chunks
-  // block -> (board, cout chunk, band); a board's 8 blocks on one XCD
-  const int bid = blockIdx.x;
-  int b, rest;
-  if (a.nboards % 8 == 0) {
-    const int x = bid & 7, k = bid >> 3;
-    b = x + 8 * (k / (2 * CO));
-    rest = k % (2 * CO);
-  } else {
-    b = bid / (2 * CO);
-    rest = bid % (2 * CO);
-  }
-  const int cg = rest >> 1, band = rest & 1;
-  if (a.active && !a.active[b]) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c0 = band * T::BCELLS;                            // the band's first cell
-  const int y0 = c0 / N;                                      // its first output row = first padded input row
-  const int pbytes = (((c0 + T::BCELLS < G::CELLS ? c0 + T::BCELLS : G::CELLS) - 1) / N - y0 + 3) * G::W * 64;
-  const int ppieces = (pbytes + 1023) >> 10;                  // (every one issued has an active lane)
-  char* const patch0 = lds;
-  char* const wring = lds + 2 * T::PB;
-  float* const sbias = reinterpret_cast<float*>(lds + 2 * T::PB + 2 * T::WSLOT);
-  float* const shw = sbias + 64;
-  const char* in = reinterpret_cast<const char*>(a.in + (long long)(a.in_idx ? a.in_idx[b] : b) * a.in_stride);
-  const char* wsrc = reinterpret_cast<const char*>(a.w + (size_t)cg * a.ci_chunks * 9 * 64 * 64);
-  if (tid < 64) {
-    sbias[tid] = a.bias[cg * 64 + tid];
-    if (a.headw)
-      for (int h = 0; h < 3; ++h) shw[h * 64 + tid] = a.headw[h * CO * 64 + cg * 64 + tid];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA counts below start from zero
-
-  // DMA (as k_tconv's, per-lane gathers): LDS byte o of a patch = (pixel
-  // o / 64 of the band's rows, physical piece (o % 64) / 16); of a weight slot
-  // = (tap o / 4096, cout row, physical piece)
-  auto issue_patch_pieces = [&](int cc, int buf, int k0, int k1) {
-    const char* src = in + (size_t)(cc >> 1) * G::P * 128;
-    const int h = cc & 1;
-    for (int k = k0; k < k1; ++k) {
-      const int ii = k * NW + wave;
-      if (ii >= ppieces) break;                          // wave-uniform
-      const int o = ii * 1024 + lane * 16;
-      if (o < pbytes) {
-        const int ql = o >> 6, pp = (o >> 4) & 3;
-        const int qg = y0 * G::W + ql;
-        const int j = pp ^ f64row(ql);
-        dma16(src + qg * 128 + ((((h << 2) + j) ^ ((qg >> 1) & 7)) << 4), lds_addr(patch0 + buf * T::PB + ii * 1024));
-      }
-    }
-  };
-  auto issue_w = [&](int s) {
-    const int cc = s / 3, ky = s - 3 * cc, h = cc & 1;
-    const char* src = wsrc + ((size_t)(cc >> 1) * 9 + ky * 3) * 64 * 64 * 2;
-    char* slot = wring + (s & 1) * T::WSLOT;
-#pragma unroll
-    for (int k = 0; k < T::WPW; ++k) {
-      const int ii = k * NW + wave;
-      const int o = ii * 1024 + lane * 16;
-      const int kx = o >> 12, r = (o >> 6) & 63, pp = (o >> 4) & 3;
-      const int j = pp ^ f64row(r);
-      dma16(src + kx * 64 * 64 * 2 + r * 128 + ((((h << 2) + j) ^ ((r >> 1) & 7)) << 4), lds_addr(slot + ii * 1024));
-    }
-  };
-  const int nsteps = 3 * CC;
-  issue_patch_pieces(0, 0, 0, T::NPW);
-  issue_w(0);
-
-  // per-lane A-fragment pixel bases in the band's patch (row-local), B offsets
-  int qb[T::MT];
-#pragma unroll
-  for (int i = 0; i < T::MT; ++i) {
-    const int m = c0 + (wave * T::MT + i) * 16 + (lane & 15);
-    qb[i] = m < G::CELLS ? (m / N - y0) * G::W + (m % N) : 0;
-  }
-  int boff[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int r = n * 16 + (lane & 15);
-    boff[n] = r * 64 + (((lane >> 4) ^ f64row(r)) << 4);
-  }
-  f32x4 acc[T::MT][4];
-#pragma unroll
-  for (int i = 0; i < T::MT; ++i)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int cc = 0; cc < CC; ++cc) {
-    const bool nextp = cc + 1 < CC;
-    const char* pbuf = patch0 + (cc & 1) * T::PB;
-    auto step = [&](auto kyc) {
-      constexpr int ky = decltype(kyc)::value;
-      const int s = cc * 3 + ky;
-      int younger = 0;
-      if (ky >= 1 && nextp) younger = T::pieces_at(ky - 1, wave, ppieces);
-      wait_vmcnt_dyn(younger);
-      lds_barrier();                                   // W(s) (and chunk cc) landed for every wave
-      if (s + 1 < nsteps) issue_w(s + 1);
-      if (nextp && ky < 2) {
-        constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
-        issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
-      }
-      const char* ws = wring + (s & 1) * T::WSLOT;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const char* wt = ws + kx * 64 * 32 * 2;
-        bf16x8 bfr[4];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bfr[n] = frag_ld(wt + boff[n]);
-#pragma unroll
-        for (int i = 0; i < T::MT; ++i) {
-          const int q = qb[i] + ky * G::W + kx;
-          const bf16x8 af = frag_ld(pbuf + q * 64 + (((lane >> 4) ^ f64row(q)) << 4));
-#pragma unroll
-          for (int n = 0; n < 4; ++n) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[n], acc[i][n], 0, 0, 0);
-        }
-      }
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-  }
-  lds_barrier();                                       // every wave's last reads done
-
-  // epilogue (k_tconv's, over the band's cells)
-  constexpr int NT = 64 * NW;
-  constexpr int ITEMS = (T::BCELLS * 8 + NT - 1) / NT;
-  const int ncell = (c0 + T::BCELLS < G::CELLS ? c0 + T::BCELLS : G::CELLS) - c0;
-  bf16* out = a.out + (long long)(a.out_idx ? a.out_idx[b] : b) * a.out_stride + (size_t)cg * G::P * 64;
-  const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
-                          : nullptr;
-  bf16x8 r8[ITEMS];
-  if (res) {
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int idx = tid + k * NT;
-      if (idx < ncell * 8) {
-        const int p = c0 + (idx >> 3), y = p / N, x = p - y * N;
-        r8[k] = *reinterpret_cast<const bf16x8*>(res + tpix((y + 1) * G::W + (x + 1), idx & 7));
-      }
-    }
-  }
-  float* set = reinterpret_cast<float*>(lds) + T::BCELLS * 68;
-  constexpr int EK = (9 * 64 + NT - 1) / NT;
-  float ev[EK];
-#pragma unroll
-  for (int k = 0; k < EK; ++k) ev[k] = 0.f;
-  if (a.etab) {
-    const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
-#pragma unroll
-    for (int k = 0; k < EK; ++k) {
-      const int i = tid + k * NT;
-      if (i < 9 * 64) ev[k] = eb[(size_t)(i >> 6) * CO * 64 + (i & 63)];
-    }
-  }
-  float* st = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < T::MT; ++i) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int pl = (wave * T::MT + i) * 16 + (lane >> 4) * 4 + r;   // band-local cell
-        if (pl < ncell) st[pl * 68 + n * 16 + (lane & 15)] = acc[i][n][r];
-      }
-  }
-  if (a.etab) {
-#pragma unroll
-    for (int k = 0; k < EK; ++k)
-      if (tid + k * NT < 9 * 64) set[tid + k * NT] = ev[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const int idx = tid + k * NT;
-    if (idx >= ncell * 8) break;
-    const int pl = idx >> 3, j = idx & 7, p = c0 + pl;
-    const int y = p / N, x = p - y * N;
-    const int q = (y + 1) * G::W + (x + 1);
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(st + pl * 68 + j * 8);
-    const f32x4 s1 = *reinterpret_cast<const f32x4*>(st + pl * 68 + j * 8 + 4);
-    float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += sbias[j * 8 + e];
-    if (a.etab) {
-      const int reg = 3 * (y == 0 ? 0 : (y == N - 1 ? 2 : 1)) + (x == 0 ? 0 : (x == N - 1 ? 2 : 1));
-      const f32x4 e0 = *reinterpret_cast<const f32x4*>(set + reg * 64 + j * 8);
-      const f32x4 e1 = *reinterpret_cast<const f32x4*>(set + reg * 64 + j * 8 + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] += e0[e]; v[e + 4] += e1[e]; }
-    }
-    const int off = tpix(q, j);
-    if (res) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += (float)r8[k][e];
-    }
-    bf16x8 o8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o8[e] = (bf16)(v[e] > 0.f ? v[e] : 0.f);
-    *reinterpret_cast<bf16x8*>(out + off) = o8;
-    if (a.headw) {
-      float h[3];
-#pragma unroll
-      for (int hh = 0; hh < 3; ++hh) {
-        float sum = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sum += shw[hh * 64 + j * 8 + e] * (float)o8[e];
-        sum += __shfl_xor(sum, 1);
-        sum += __shfl_xor(sum, 2);
-        sum += __shfl_xor(sum, 4);
-        h[hh] = sum;
-      }
-      if (j == 0) {
-        float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
-        hp[0] = h[0];
-        hp[G::CS] = h[1];
-        hp[2 * G::CS] = h[2];
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------

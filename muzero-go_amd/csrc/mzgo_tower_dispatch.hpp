@@ -38,15 +38,7 @@ int tower_stamps_n19(unsigned long long* out);
 template <int N>
 struct TLaunch {
   static hipError_t conv(const TConvArgs& a, hipStream_t s) {
-    // 8 waves (2 per SIMD) unless MZGO_TCONV_WAVES=4 (A/B runs); 19x19 with
-    // MZGO_TCONV_V2=1: two workgroups per CU (k_tconv2, measured slower)
-    if constexpr (N == 19) {
-      static const bool v2 = [] { const char* e = getenv("MZGO_TCONV_V2"); return e && atoi(e) == 1; }();
-      if (v2) {
-        hipLaunchKernelGGL((k_tconv2<N>), dim3(a.nboards * a.co_chunks * 2), dim3(256), 0, s, a);
-        return hipGetLastError();
-      }
-    }
+    // 8 waves (2 per SIMD) unless MZGO_TCONV_WAVES=4 (A/B runs)
     static const int nw = [] { const char* e = getenv("MZGO_TCONV_WAVES"); return e && atoi(e) == 4 ? 4 : 8; }();
     if (nw == 4)
       hipLaunchKernelGGL((k_tconv<N, 4>), dim3(a.nboards * a.co_chunks), dim3(256), 0, s, a);
