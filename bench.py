@@ -265,7 +265,8 @@ def tower_main(args, world, rank, local, cpu_ref):
     sims = c1["simulations"] - c0["simulations"]
     moves = c1["moves"] - c0["moves"]
     if world > 1:
-        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64,
+                         device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -329,6 +330,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N>1 path on a one-GPU box (never the driver's runs):
+    # MZGO_SHARE_DEVICE=1 puts every rank on cuda:0, MZGO_DIST_BACKEND=gloo
+    # replaces RCCL (which refuses two ranks on one GPU)
+    backend = os.environ.get("MZGO_DIST_BACKEND", "nccl")
+    if os.environ.get("MZGO_SHARE_DEVICE") == "1":
+        local = 0
     cpu_ref = None
     if world == 1 and not args.no_cpu_baseline:
         # before the GPU is initialised: the baseline spawns worker processes
@@ -337,7 +344,10 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     if args.config == 5:
         tower_main(args, world, rank, local, cpu_ref)
         return
@@ -410,7 +420,8 @@ def main():
     avg_kern_s = sum(kern_ms) / launches / 1e3
 
     if world > 1:
-        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64,
+                         device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)

@@ -72,6 +72,8 @@ def gather_packed(buf, dst=0, group=None, to_host=True):
     over RCCL for CUDA tensors); host numpy arrays there if ``to_host``."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
+    if buf.is_cuda and dist.get_backend(group) == "gloo":
+        buf = buf.cpu()                       # gloo gathers host tensors (CPU tests, one-GPU rehearsals)
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
     dist.gather(buf, parts, dst=dst, group=group)
     if rank != dst:

@@ -177,13 +177,20 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one-GPU rehearsal (as bench.py): every rank on cuda:0, gloo for RCCL
+    if os.environ.get("MZGO_SHARE_DEVICE") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
 
         from . import distributed as mdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("MZGO_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     N = args.board_size
     net = MuZeroNet(args.latent_dim, N * N + 1).to(f"cuda:{local}").eval()
