@@ -251,9 +251,25 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
   };
   STAMP_T(tpro);
 
+  // The first A fragments of kernel rows 1 and 2 are read at the end of the
+  // previous step, before its barrier (same patch buffer, no hazard): 26.5 ->
+  // 26.2 us per conv (MZGO_TCONV_NOAPRE=1 to read them after the barrier)
+#ifdef MZGO_TCONV_NOAPRE
+  constexpr bool APRE = false;
+#else
+  constexpr bool APRE = true;
+#endif
   for (int cc = 0; cc < CC; ++cc) {
     const bool nextp = cc + 1 < CC;
     const char* pbuf = patch0 + (cc & 1) * T::PB;
+    bf16x8 afn[T::ADIST > 0 ? T::ADIST : 1][2];
+    // A fragments of group g (tap kx, tile i) of kernel row ky
+    auto frag_a = [&](int kyv, int kx, int i, bf16x8 (&d)[2]) {
+      const int q = qb[i] + kyv * G::W + kx;
+      const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
+      d[0] = frag_ld(pbuf + off);
+      d[1] = frag_ld(pbuf + (off ^ 64));
+    };
     auto step = [&](auto kyc) {
       constexpr int ky = decltype(kyc)::value;
       const int s = cc * 3 + ky;
@@ -263,14 +279,31 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
       if (ky >= 1 && ky - 1 < 2 && nextp) younger = T::pieces_at(ky - 1, wave);
       wait_vmcnt_dyn(younger);
       STAMP_T(ts1);
-      lds_barrier();                                   // W(s) (and chunk cc) landed for every wave
-      STAMP_T(ts2);
-      if (s + 1 < nsteps) issue_w(s + 1);
-      if (nextp && ky < 2) {
-        constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
-        issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
+      // W(s) (and chunk cc) landed for every wave; this wave's ring reads
+      // done (with APRE the pre-read A fragments, issued last, may stay in flight)
+      if constexpr (APRE && ky > 0) {
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * T::ADIST) : "memory");
+        __builtin_amdgcn_s_barrier();
+      } else {
+        lds_barrier();
       }
-      if (s == nsteps - 1) touch_epilogue();
+      STAMP_T(ts2);
+      auto issue_dma = [&]() {
+        if (s + 1 < nsteps) issue_w(s + 1);
+        if (nextp && ky < 2) {
+          constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
+          issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
+        }
+        if (s == nsteps - 1) touch_epilogue();
+      };
+      // the step's first fragment reads go out before this wave's DMA issue
+      // (26.4 vs 27.0 us per conv; MZGO_TCONV_DMA_FIRST=1 for the old order)
+#ifdef MZGO_TCONV_DMA_FIRST
+      constexpr bool reads_first = false;
+#else
+      constexpr bool reads_first = true;
+#endif
+      if constexpr (!reads_first) issue_dma();
       // One basic block per step (no per-tile branch: a wave past the last
       // tile multiplies a clamped tile and drops it in the epilogue), as
       // groups g = (tap kx, tile i): each group first issues the A fragments
@@ -295,7 +328,13 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
         af[g % (AD + 1)][1] = frag_ld(pbuf + (off ^ 64));
       };
       load_b(0, bf[0]);
-      static_for<AD>([&](auto gc) { load_a(gc); });
+      if constexpr (APRE && ky > 0) {
+#pragma unroll
+        for (int g = 0; g < AD; ++g) { af[g][0] = afn[g][0]; af[g][1] = afn[g][1]; }
+      } else {
+        static_for<AD>([&](auto gc) { load_a(gc); });
+      }
+      if constexpr (reads_first) issue_dma();
       auto group = [&](auto gc) {
         constexpr int g = decltype(gc)::value, kx = g / T::MT, i = g % T::MT;
         if constexpr (i == 0 && kx + 1 < 3) load_b(kx + 1, bf[(kx + 1) & 1]);
@@ -312,6 +351,11 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       };
       static_for<NG>([&](auto gc) { group(gc); });
+      if constexpr (APRE && ky < 2) {
+        __builtin_amdgcn_sched_barrier(0);             // the pre-reads are this step's last LDS ops
+#pragma unroll
+        for (int g = 0; g < AD; ++g) frag_a(ky + 1, g / T::MT, g % T::MT, afn[g]);
+      }
       STAMP_T(ts3);
 #ifdef MZGO_TCONV_STAMPS
       acc_wait += ts1 - ts0; acc_bar += ts2 - ts1; acc_mfma += ts3 - ts2;
