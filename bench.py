@@ -303,12 +303,14 @@ def main():
                          "5: 19x19 / 20-block residual nets / 1600 sims / 64 games (BASELINE configs[4])")
     ap.add_argument("--blocks", type=int, default=20, help="residual blocks (config 5)")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10, help="whole self-play epochs timed")
-    ap.add_argument("--warmup", type=int, default=1, help="untimed epochs")
-    ap.add_argument("--board-size", type=int, default=9)
-    ap.add_argument("--games", type=int, default=256, help="parallel games per GPU")
-    ap.add_argument("--sims", type=int, default=200)
-    ap.add_argument("--latent-dim", type=int, default=96)
+    # defaults per config (2: 10 / 1 / 9 / 256 / 200 / 96; 5: 2 / 1 / 19 / 64 / 1600 / 256), filled below
+    # only where the option is not given
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: whole self-play epochs)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps")
+    ap.add_argument("--board-size", type=int, default=None)
+    ap.add_argument("--games", type=int, default=None, help="parallel games per GPU")
+    ap.add_argument("--sims", type=int, default=None)
+    ap.add_argument("--latent-dim", type=int, default=None)
     ap.add_argument("--dynamics", choices=["factored", "direct"], default="factored",
                     help="factored: one conv per parent, children as relu(Y + E[a]) (mzgo_expand.hpp); "
                          "direct: a dynamics conv per simulation, as the reference computes it")
@@ -319,13 +321,11 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="oracle processes for cpu_baseline (the GPU box's CPU share is 16)")
     args = ap.parse_args()
-    if args.config == 5:
-        # config 5's sizes unless given explicitly
-        defaults = dict(board_size=9, games=256, sims=200, latent_dim=96, steps=10, warmup=1)
-        c5 = dict(board_size=19, games=64, sims=1600, latent_dim=256, steps=2, warmup=1)
-        for k, v in c5.items():
-            if getattr(args, k) == defaults[k]:
-                setattr(args, k, v)
+    defaults = {2: dict(board_size=9, games=256, sims=200, latent_dim=96, steps=10, warmup=1),
+                5: dict(board_size=19, games=64, sims=1600, latent_dim=256, steps=2, warmup=1)}[args.config]
+    for k, v in defaults.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

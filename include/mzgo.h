@@ -148,7 +148,10 @@ int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
 /* Up to ``moves`` consecutive moves of every unfinished slot in ONE launch
  * (each slot stops at its game's end); the records and RNG streams are those
- * of ``moves`` mzgo_selfplay_move calls.  moves = max_moves plays whole games. */
+ * of ``moves`` mzgo_selfplay_move calls.  moves = max_moves plays whole games.
+ * Tower engines (tower = 1) run a move as a sequence of launches; they check
+ * the slots' status every 4 moves (synchronising the stream) and stop
+ * enqueueing once every game has ended. */
 int mzgo_selfplay_moves(mzgo_engine* eng, int moves, void* stream);
 
 /* Arena (main.py:526-611, SelfPlayEvaluator): like mzgo_selfplay_move, but

@@ -687,7 +687,18 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
     TowerHost& t = *e->tower;
     hipStream_t s = (hipStream_t)stream;
     const SearchParams sp = e->search_params();
+    std::vector<int> st(e->G);
     for (int k = 0; k < moves; ++k) {
+      // a tower move is ~43 launches per simulation, so once every game has
+      // ended the remaining moves are not enqueued at all: every 4 moves the
+      // host reads the slots' status (one small copy per ~4 x S towers)
+      if (k > 0 && k % 4 == 0) {
+        HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        bool any = false;
+        for (int v : st) any |= v == 0;
+        if (!any) break;
+      }
       HIPCHK(t.ts->obs(t.TA, sp, pp, e->E, e->G, s));
       HIPCHK(t.root_phase(sp, e->E, e->noise, (long long)e->M * e->A, 1, s));
       HIPCHK(t.simulations(sp, e->E, s));

@@ -105,6 +105,9 @@ struct Smem {
   int misc[8];
   int bc[8];                                             // broadcast slots
   // a batching configuration's buffers were sized to the union's budget
+  // a batching configuration's buffers were sized to the union's budget (a
+  // non-batching one may grow the union: the kernels assert the whole Smem
+  // fits one CU's LDS)
   static_assert(!ExpandLds<G, G::CINMAX * G::CPAD>::BATCH ||
                     sizeof(ExpandLds<G, G::CINMAX * G::CPAD>) <= sizeof(float) * G::CINMAX * G::CPAD,
                 "the batched expansion's LDS must fit the conv staging it overlays");
@@ -276,6 +279,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                                  float* scratch) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int b = blockIdx.x;
   const float* o = obs + (size_t)b * 6 * G::CELLS;
@@ -293,6 +297,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                                    float* value, float* logits, int* err) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int b = blockIdx.x;
   int64_t a = action[b];
@@ -482,11 +487,22 @@ __device__ __forceinline__ bool shared_jobs(const SearchParams& sp) {
 
 // A job's batch number (unique within a launch: the host zeroes the jobs
 // before it) with the claim word and the done counter reset for it.  Thread 0.
-__device__ __forceinline__ unsigned job_begin(const JobView& J, unsigned first = 0) {
+//
+// The claim word is batch << 32 | total << 16 | next: a claim is decided by
+// the word alone, never by the job's info block.  A helper that acquired
+// batch s can read info rows the game's workgroup is already rewriting for
+// s + 1 (the game claims every unit of s itself when no helper comes, waits
+// for them and begins s + 1 at once); its CAS on the word of s then fails
+// whatever total that info says, because s's word is exhausted (next >=
+// total) before the game can begin s + 1, and the new word carries s + 1.
+// A successful claim of s therefore means s is still open, so every info
+// row the helper read belongs to s, and no stale done add can reach s + 1.
+__device__ __forceinline__ unsigned job_begin(const JobView& J, int total, unsigned first = 0) {
   const unsigned bseq = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   if (threadIdx.x == 0) {
     __hip_atomic_store(J.done(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32 | first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32 | (unsigned)total << 16 | first, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   return bseq;
 }
@@ -521,10 +537,11 @@ __device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned
     int c0 = -1;
     unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {                                       // (a failed CAS means another claim succeeded)
-      if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFFFFFu) >= total) break;
+      // (the word's own total decides: see job_begin; `total` is the caller's copy)
+      if ((unsigned)(c >> 32) != bseq || (int)(c & 0xFFFFu) >= (int)((c >> 16) & 0xFFFFu)) break;
       if (__hip_atomic_compare_exchange_strong(J.claim(), &c, c + step, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
-        c0 = (int)(c & 0xFFFFFFFFu);
+        c0 = (int)(c & 0xFFFFu);
         break;
       }
     }
@@ -573,7 +590,7 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
                                             int leaf, int net, const float* src, float* dst,
                                             Stamp* st = nullptr, int par = -1, int act = 0, Pre pre = Pre{}) {
   const JobView J = job_of<G>(E, g);
-  const unsigned bseq = job_begin(J);
+  const unsigned bseq = job_begin(J, Wino<G>::NSTRIP);
   if (threadIdx.x == 0) {
     int* info = J.info();
     info[0] = Wino<G>::NSTRIP; info[1] = par; info[2] = leaf; info[3] = net; info[4] = par >= 0 ? 2 : 1;
@@ -619,7 +636,7 @@ __device__ __forceinline__ void rep_shared(Smem<G>& sm, const NetParams& np, con
   const JobView J = job_of<G>(E, g);
   float* pool = pool_of<G>(E, g);
   float* lat = pool + (size_t)(E.S + 1) * G::C * G::CS;
-  const unsigned bseq = job_begin(J);
+  const unsigned bseq = job_begin(J, Wino<G>::NSTRIP);
   if (threadIdx.x == 0) {
     int* info = J.info();
     info[0] = Wino<G>::NSTRIP; info[1] = 0; info[2] = 0; info[3] = net; info[4] = k == 2 ? 4 : 5;
@@ -740,7 +757,7 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
                                                     Wait pre_wait = Wait{}) {
   auto& L = sm.u.f;
   const JobView J = job_of<G>(E, g);
-  const unsigned bseq = job_begin(J);
+  const unsigned bseq = job_begin(J, B);
   // the job first (geometry, the root's mask, the actions known already:
   // i0 of them), then the picks (pick_all, wave 0; tagged entries: a helper
   // that claims a round before they are out waits for its entry)
@@ -1239,7 +1256,7 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   const bool shared = vp.shared;
   if (shared) {
     const JobView J = job_of<G>(E, g);
-    const unsigned bseq = job_begin(J, preloaded ? 1u : 0u);
+    const unsigned bseq = job_begin(J, ngroups, preloaded ? 1u : 0u);
     if (threadIdx.x == 0) {
       int* info = J.info();
       info[0] = ngroups; info[1] = nid; info[2] = leaf; info[3] = gs; info[4] = 3;
@@ -1753,6 +1770,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                       int move_index, int* out_visits, double* out_value) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   const int g = blockIdx.x;
   const float* o = root_obs + (size_t)g * 6 * G::CELLS;
@@ -1820,6 +1838,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                           int* status, double* winner, double komi) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   const int g = blockIdx.x;
   const int a = actions[g];
   if (a < 0) return;
@@ -2026,8 +2045,12 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
                                                              SearchParams sp, PlayParams pp, EngineArrays E) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
+  static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   // blocks past the games are helper workgroups (batch_expand_shared): helper h
-  // serves game h % games (the same XCD under round-robin dispatch)
+  // serves game h % games.  Under round-robin dispatch that is the game's XCD
+  // when games % 8 == 0 (every bench and test shape: 64, 256); otherwise a
+  // helper may sit on another XCD -- a speed matter only, the job hand-offs
+  // are agent-scope release / acquire and placement-independent.
   const int games = gridDim.x - sp.helpers;
   if ((int)blockIdx.x >= games) {
     if constexpr (Smem<G>::GLOBAL_Y && G::WINO) {

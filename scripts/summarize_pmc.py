@@ -49,10 +49,21 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
 c = mean
 dur = out["avg_duration_ms"] / 1e3
 if "GRBM_GUI_ACTIVE" in c:
-    clk = c["GRBM_GUI_ACTIVE"] / 8 / dur
+    # GRBM_GUI_ACTIVE / 8 XCDs / duration reads HIGH on dispatches shorter
+    # than ~0.3 ms (MI355X_MICROARCH.md, DVFS give-back): k_tconv's 26 us
+    # launches gave 3.12 GHz.  The clock used is that quotient only for
+    # dispatches >= 0.3 ms, and never above the chip's 2.4 GHz maximum; for
+    # shorter ones it is 2.4 GHz, so every busy fraction below is a LOWER
+    # bound (the in-kernel s_memtime clock, ~2.1 GHz on k_tconv, would give
+    # fractions ~14 % higher).
+    grbm_clk = c["GRBM_GUI_ACTIVE"] / 8 / dur
+    clk = min(grbm_clk, 2.4e9) if dur >= 0.3e-3 else 2.4e9
     cu_cycles = 256 * clk * dur
     out["derived"] = {
         "effective_clock_GHz": clk / 1e9,
+        "grbm_quotient_GHz": grbm_clk / 1e9,
+        "clock_source": ("GRBM_GUI_ACTIVE / 8 / duration (dispatch >= 0.3 ms), capped at 2.4 GHz"
+                         if dur >= 0.3e-3 else "2.4 GHz (dispatch < 0.3 ms: the GRBM quotient reads high)"),
         "valu_issue_frac": c.get("SQ_INSTS_VALU", 0) / (2 * cu_cycles),
         "mfma_busy_frac": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (4 * cu_cycles),
         "mfma_insts_per_launch": c.get("SQ_INSTS_MFMA", 0),
@@ -61,7 +72,7 @@ if "GRBM_GUI_ACTIVE" in c:
         "wave_wait_any_share": c.get("SQ_WAIT_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
         "wave_issue_stall_share": c.get("SQ_WAIT_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
         "wave_active_share": c.get("SQ_ACTIVE_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
-        "note": "fractions of CU-cycles at the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration); "
+        "note": "fractions of CU-cycles at effective_clock_GHz (see clock_source); "
                 "VALU peak 2 wave-instr/clk/CU, MFMA busy summed over 4 SIMDs, LDS array one cycle/clk/CU; "
                 "wave shares of SQ_WAVE_CYCLES (quad-cycles, as the SQ_WAIT_*/ACTIVE_* counters)",
     }

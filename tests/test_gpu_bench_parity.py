@@ -111,6 +111,64 @@ def _replay_all(hists, N, S, counters):
         assert float(h.final_reward) == (float(gg.winning(st)) if ended else 0.0)
 
 
+def _records(eng):
+    """Every slot's record, truncated to its length, from one packed copy."""
+    from mzgo.distributed import slot_records, unpack
+    arrays = unpack(pack_engine_host(eng), eng.G, eng.M, eng.N)
+    return [slot_records(arrays, g) for g in range(eng.G)], arrays
+
+
+def pack_engine_host(eng):
+    from mzgo.distributed import pack_engine
+    return pack_engine(eng).cpu().numpy()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("N,G,S,epoch", [(9, 256, 200, 3), (19, 64, 800, 1)],
+                         ids=["9x9_g256_s200", "19x19_g64_s800"])
+def test_whole_game_launch_equals_per_move_launches(N, G, S, epoch):
+    """bench.py plays an epoch as ONE k_selfplay_move launch (the move loop
+    inside the kernel: the build that spills); the oracle tests
+    above drive one launch per move.  Both launch structures must leave
+    byte-identical records (observations, actions, values, policies, rewards,
+    lengths, status, final reward) and identical counters at the bench's own
+    sizes -- 9x9 / 256 / 200 and 19x19 / 64 / 800 with its 3 helper
+    workgroups per game -- so the oracle chain covers the bench's launch."""
+    net = _net(N)
+    sp = __import__("mzgo").SelfPlay(net, G, S, seed=SEED)
+    eng = sp.engine
+    M = sp.max_moves
+
+    def run(per_move):
+        c0 = eng.counters()
+        sp.reset(epoch=epoch)
+        if per_move:
+            for _ in range(M):
+                sp.move()
+        else:
+            sp.move(M)                       # exactly bench.py's one_epoch()
+        c1 = eng.counters()
+        recs, arrays = _records(eng)
+        c = {k: c1[k] - c0[k] for k in ("simulations", "moves", "games_finished", "dynamics_convs")}
+        c["playing"] = c1["playing"]
+        return recs, arrays, c
+
+    whole, wa, cw = run(False)
+    per, pa, cp = run(True)
+    assert cw == cp, (cw, cp)
+    assert cw["playing"] == 0 and cw["games_finished"] == G
+    np.testing.assert_array_equal(wa["meta"], pa["meta"])
+    np.testing.assert_array_equal(wa["status"], pa["status"])
+    np.testing.assert_array_equal(wa["final"].view(np.uint64), pa["final"].view(np.uint64))
+    for g in range(G):
+        a, b = whole[g], per[g]
+        assert a["length"] == b["length"], g
+        for k in ("stones", "invd", "flags", "action"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"game {g} {k}")
+        for k in ("value", "policy", "reward"):      # f64: bit patterns
+            np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64), err_msg=f"game {g} {k}")
+
+
 CONFIGS = [
     # N, G, S, {move: games} sampled for the oracle tree comparison
     (9, 256, 200, {0: [0, 131], 7: [5, 200], 20: [17, 255], 41: [3, 64], 66: [99], 80: [128]}),
