@@ -36,9 +36,10 @@ def mfma_per_conv(N, cin, cout):
     return 9 * (cin // 4) * (cout // 16) * ((N * N + 15) // 16)
 
 
-def cpu_baseline(N, C, S, budget_s=12.0, blocks=None):
+def cpu_baseline(N, C, S, budget_s=12.0, blocks=None, threads=1):
     """The oracle (CPU restatement of self_play.py's MCTS, batch-1 torch net,
-    object tree) timed on this host with one thread, on a bounded sample.
+    object tree) timed on this host with ``threads`` intra-op threads (1: the
+    per-process leg), on a bounded sample.
     blocks: the residual-tower network of config 5 (oracle/resnet.py, fp32)."""
     import numpy as np
 
@@ -48,7 +49,7 @@ def cpu_baseline(N, C, S, budget_s=12.0, blocks=None):
     from oracle.weights import deterministic_state_dict
     from oracle import gogame
 
-    torch.set_num_threads(1)
+    torch.set_num_threads(threads)
     A = N * N + 1
     if blocks is None:
         net = OracleNet(deterministic_state_dict(C, A, 0))
@@ -77,13 +78,17 @@ def cpu_baseline(N, C, S, budget_s=12.0, blocks=None):
             st = gogame.init_state(N)
     dt = time.perf_counter() - t0
     net_name = "batch-1 net" if blocks is None else f"{blocks}-block residual net (fp32), batch 1"
-    return {"value": sims / dt, "unit": "sims/s", "cores": 1, "kind": "port",
-            "sample": f"{moves} moves, {sims} sims, {N}x{N}, one game, 1 thread, {dt:.1f} s "
+    return {"value": sims / dt, "unit": "sims/s", "cores": threads, "kind": "port",
+            "sample": f"{moves} moves, {sims} sims, {N}x{N}, one game, {threads} thread(s), {dt:.1f} s "
                       f"(oracle MCTS + torch-CPU {net_name}; host has {os.cpu_count()} cpus)"}
 
 
 def _cpu_worker(a):
     return cpu_baseline(*a)
+
+
+def _cpu_worker_threads(a):
+    return cpu_baseline(*a[:4], blocks=a[4], threads=a[5])
 
 
 def cpu_baseline_procs(N, C, S, budget_s, procs, blocks=None):
@@ -95,9 +100,14 @@ def cpu_baseline_procs(N, C, S, budget_s, procs, blocks=None):
         return cpu_baseline(N, C, S, budget_s, blocks)
     with mp.get_context("spawn").Pool(procs) as pool:
         res = pool.map(_cpu_worker, [(N, C, S, budget_s, blocks)] * procs)
+    # BASELINE.md's other CPU row: ONE process using every thread of the
+    # share (the reference run as-is: one game, torch's intra-op threads)
+    with mp.get_context("spawn").Pool(1) as pool:
+        one = pool.map(_cpu_worker_threads, [(N, C, S, budget_s / 2, blocks, procs)])[0]
     total = sum(r["value"] for r in res)
     return {"value": total, "unit": "sims/s", "cores": procs, "kind": "port",
             "single_core_value": res[0]["value"],
+            "one_process_all_threads": {"value": one["value"], "threads": procs, "sample": one["sample"]},
             "sample": f"{procs} processes x 1 thread, each one {N}x{N} game at {S} sims/move for "
                       f"{budget_s:.0f} s (oracle MCTS + torch-CPU batch-1 net; host has {os.cpu_count()} cpus)"}
 
@@ -122,6 +132,22 @@ def pmc_summary(workload, dynamics, moves_per_launch):
             or p.get("moves_per_launch", 1) != moves_per_launch):
         return None
     return p
+
+
+def phases_summary(workload, moves_per_launch):
+    """Per-phase shares of an epoch (select / expand / conv /
+    replay / root / board / representation) and the epoch's tail, from the
+    -DMZGO_STAMPS build of the same workload (scripts/phases.py ->
+    profiles/<tag>_phases.json; in the timed kernel no stamp executes)."""
+    path = os.path.join(ROOT, "profiles", "latest_phases.json")
+    if moves_per_launch != 0 or not os.path.exists(path):
+        return None
+    p = json.load(open(path))
+    if p.get("workload") != workload:
+        return None
+    return {"shares": {k: round(v, 4) for k, v in p["shares"].items()},
+            "tail_idle_cu_share": round(p["tail"]["idle_cu_share"], 4),
+            "source": f"profiles/{p['tag']}_phases.json"}
 
 
 def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch):
@@ -296,6 +322,92 @@ def tower_main(args, world, rank, local, cpu_ref):
         dist.destroy_process_group()
 
 
+def refill_main(args, net, world, rank, local, cpu_ref):
+    """Refill configuration (the epoch tail): R engines of G game
+    slots each, engine r on HIP stream r; step i plays one whole epoch of G
+    games on engine i % R.  Kernels on different streams run concurrently, so
+    the workgroups of epoch i + 1 start on the CUs that epoch i's finished
+    games free (one game workgroup fills a CU's LDS), instead of those CUs
+    idling until epoch i's slowest game ends; stream order keeps each
+    engine's epochs sequential.  Same games, kernel and records as the
+    headline (game ids (rank * R + r) * G + slot, epoch keys distinct); value
+    = all simulations / wall time."""
+    import mzgo
+    N, C, S, G, R = args.board_size, args.latent_dim, args.sims, args.games, args.refill
+    sps = [mzgo.SelfPlay(net, G, S, seed=1234, game_base=(rank * R + r) * G, dynamics=args.dynamics)
+           for r in range(R)]
+    M = sps[0].max_moves
+    streams = [torch.cuda.Stream() for _ in range(R)]
+    ev = []
+    step_no = [0]
+
+    def one_epoch(record):
+        i = step_no[0]
+        r = i % R
+        with torch.cuda.stream(streams[r]):
+            if record:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(streams[r])
+            sps[r].reset(epoch=i)
+            sps[r].move(M)
+            if record:
+                b.record(streams[r])
+                ev.append((a, b))
+        step_no[0] += 1
+
+    for _ in range(max(args.warmup, R)):
+        one_epoch(False)
+    torch.cuda.synchronize()
+    c0 = [sp.engine.counters() for sp in sps]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_epoch(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    c1 = [sp.engine.counters() for sp in sps]
+    sims = sum(b["simulations"] - a["simulations"] for a, b in zip(c0, c1))
+    moves = sum(b["moves"] - a["moves"] for a, b in zip(c0, c1))
+    convs = sum(b["dynamics_convs"] - a["dynamics_convs"] for a, b in zip(c0, c1))
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    if world > 1:
+        t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64,
+                         device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
+    if rank == 0:
+        workload = f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move"
+        counts = dict(launches=len(kern_ms), sims=sims / world, moves=moves / world, convs=convs)
+        roof = roofline(N, C, S, G, counts, sum(kern_ms) / len(kern_ms) / 1e3, args.dynamics,
+                        workload + f", refill {R}", 0)
+        out = {
+            "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {S} sims/move "
+                      f"(refill configuration)",
+            "value": sims / dt, "unit": "sims/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
+            "moves_per_s": moves / dt,
+            "config": {"workload": workload, "step": f"one whole self-play epoch of {G} games/GPU, epochs on "
+                                                     f"{R} engines / HIP streams overlapping (refill)",
+                       "board_size": N, "latent_dim": C, "games_per_gpu": G, "sims_per_move": S,
+                       "parallelism": f"game-sharded x{world}", "compat": "reference", "dynamics": args.dynamics,
+                       "refill": R},
+            "roofline": roof,
+        }
+        if cpu_ref is not None:
+            out["cpu_baseline"] = cpu_ref
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
@@ -316,6 +428,10 @@ def main():
                          "direct: a dynamics conv per simulation, as the reference computes it")
     ap.add_argument("--moves-per-launch", type=int, default=0,
                     help="moves of every game per k_selfplay_move launch (0 = whole games)")
+    ap.add_argument("--refill", type=int, default=0,
+                    help="R >= 2: a separate configuration (not the headline): R engines of G slots on R HIP "
+                         "streams play consecutive epochs, so CUs a finished game frees start the next epoch's "
+                         "games instead of idling while the epoch's slowest games finish (the epoch tail)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
@@ -362,6 +478,9 @@ def main():
     if world > 1:
         from mzgo import distributed as mdist
         mdist.broadcast_weights(net)                      # one RCCL broadcast, untimed
+    if args.refill >= 2:
+        refill_main(args, net, world, rank, local, cpu_ref)
+        return
     sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G, dynamics=args.dynamics)
     eng = sp.engine
     M = sp.max_moves
@@ -454,6 +573,9 @@ def main():
                        "dynamics": args.dynamics},
             "roofline": roof,
         }
+        ph = phases_summary(workload, args.moves_per_launch) if args.dynamics == "factored" else None
+        if ph is not None:
+            out["phases"] = ph
         if cpu_ref is not None:
             out["cpu_baseline"] = cpu_ref
         print(json.dumps(out))

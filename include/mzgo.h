@@ -170,6 +170,21 @@ int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stre
  * simulation step's 2*res_blocks+1 conv launches, on the launch stream -- then
  * switch the timing on (enable = 1) or off. */
 int mzgo_tower_timing(mzgo_engine* eng, int enable, double* tower_ms_host, int64_t* towers_host);
+
+/* Trainer backward of the dynamics conv (main.py:478-482's loss.backward()
+ * through DynamicsNetwork.forward, main.py:97-103; replaces
+ * torch.nn.grad.conv2d_input / conv2d_weight in the trainer's HIP autograd
+ * Function).  Forward: out = relu(conv3x3(latent + emb[action]) + bias),
+ * padding 1.  In: grad_out, out, latent [B][C][N][N] f32, action [B] i64,
+ * emb [A][C], weight [C][C][3][3].  Out: grad_latent [B][C][N][N] (= the
+ * conv input's gradient), grad_weight [C][C][3][3], grad_bias [C]; fp32 MFMA,
+ * deterministic.  C a multiple of 16, 2 <= N <= 19; workspace of at least
+ * mzgo_dyn_conv_backward_workspace(B, C) bytes (device). */
+int mzgo_dyn_conv_backward_workspace(int B, int C, int64_t* bytes_host);
+int mzgo_dyn_conv_backward(const float* grad_out, const float* out, const float* latent, const int64_t* action,
+                           const float* emb, const float* weight, int B, int C, int N, float* grad_latent,
+                           float* grad_weight, float* grad_bias, void* workspace, int64_t workspace_bytes,
+                           void* stream);
 /* Test hook: use injected Dirichlet samples f64 [G][max_moves][A] (device,
  * caller-owned, must outlive the moves) instead of the counter-RNG sampler;
  * NULL restores sampling. */

@@ -18,6 +18,12 @@ namespace mzgo {
 extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96, kernels_n6_c128,
     kernels_n6_c64;
 
+// the trainer's backward kernels (mzgo_train.hip)
+size_t dyn_bwd_workspace_bytes(int B, int C);
+hipError_t dyn_conv_backward(const float* g, const float* out, const float* latent, const int64_t* action,
+                             const float* emb, const float* w, int B, int C, int N, float* gx, float* gw,
+                             float* gb, void* workspace, hipStream_t s);
+
 const KernelSet* find_kernels(int N, int C) {
   static const KernelSet* all[] = {&kernels_n5_c96, &kernels_n6_c96, &kernels_n9_c96, &kernels_n19_c96,
                                    &kernels_n6_c128, &kernels_n6_c64};
@@ -733,6 +739,27 @@ int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* str
   pp.arena = 1;
   pp.moves = moves;
   return launch_selfplay(e, opponent->np, pp, (hipStream_t)stream);
+}
+
+int mzgo_dyn_conv_backward_workspace(int B, int C, int64_t* bytes_host) {
+  if (B < 1 || C < 16 || C % 16 || !bytes_host) return fail(MZGO_EINVAL, "bad argument (B=%d, C=%d)", B, C);
+  *bytes_host = (int64_t)dyn_bwd_workspace_bytes(B, C);
+  return MZGO_OK;
+}
+
+int mzgo_dyn_conv_backward(const float* grad_out, const float* out, const float* latent, const int64_t* action,
+                           const float* emb, const float* weight, int B, int C, int N, float* grad_latent,
+                           float* grad_weight, float* grad_bias, void* workspace, int64_t workspace_bytes,
+                           void* stream) {
+  if (!grad_out || !out || !latent || !action || !emb || !weight || !grad_latent || !grad_weight || !grad_bias ||
+      !workspace || B < 1 || C < 16 || C % 16 || N < 2 || N > 19)
+    return fail(MZGO_EINVAL, "bad argument (B=%d, C=%d, N=%d)", B, C, N);
+  if (workspace_bytes < (int64_t)dyn_bwd_workspace_bytes(B, C))
+    return fail(MZGO_EINVAL, "workspace too small: %lld < %lld bytes", (long long)workspace_bytes,
+                (long long)dyn_bwd_workspace_bytes(B, C));
+  HIPCHK(dyn_conv_backward(grad_out, out, latent, action, emb, weight, B, C, N, grad_latent, grad_weight, grad_bias,
+                           workspace, (hipStream_t)stream));
+  return MZGO_OK;
 }
 
 int mzgo_tower_timing(mzgo_engine* e, int enable, double* tower_ms, int64_t* towers) {

@@ -37,6 +37,29 @@ __device__ __forceinline__ NetParams select_params(bool b, const NetParams& x, c
   return n;
 }
 
+// A kernel-argument pointer made opaque to the optimizer at this point of the
+// program (an empty asm on its SGPR pair) and re-marked global: address
+// arithmetic derived from it cannot be hoisted above the point.  The
+// whole-game k_selfplay_move launders its arguments at the head of every move,
+// so per-lane addresses are formed per move instead of once at the kernel
+// entry and kept (spilled) across the whole game.
+template <class T>
+__device__ __forceinline__ T* launder_global(T* p) {
+  unsigned long long x = reinterpret_cast<unsigned long long>(p);
+  asm volatile("" : "+s"(x));
+  return (T*)reinterpret_cast<__attribute__((address_space(1))) T*>(x);
+}
+__device__ __forceinline__ NetParams launder_params(const NetParams& n) {
+  NetParams r;
+#define MZGO_L(f) r.f = launder_global(n.f);
+  MZGO_L(w_conv1) MZGO_L(b_conv1) MZGO_L(w_conv2) MZGO_L(b_conv2) MZGO_L(w_conv3) MZGO_L(b_conv3)
+  MZGO_L(w_dyn) MZGO_L(b_dyn) MZGO_L(emb) MZGO_L(head_w) MZGO_L(etab)
+  MZGO_L(hs.reward_b) MZGO_L(hs.fc1_w) MZGO_L(hs.fc1_b) MZGO_L(hs.fc2_w) MZGO_L(hs.fc2_b)
+  MZGO_L(hs.value_b) MZGO_L(hs.vfc_w) MZGO_L(hs.vfc_b) MZGO_L(hs.policy_b) MZGO_L(hs.pass_logit)
+#undef MZGO_L
+  return r;
+}
+
 // Per-slot device state of an engine (sizes fixed at engine creation).
 struct EngineArrays {
   int S;                 // simulations per move this engine was sized for
@@ -72,6 +95,17 @@ struct EngineArrays {
                                  //     3: dynamics convs run (factored: one per new parent)
   unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
 };
+
+__device__ __forceinline__ EngineArrays launder_arrays(const EngineArrays& e) {
+  EngineArrays r = e;
+#define MZGO_L(f) r.f = launder_global(e.f);
+  MZGO_L(pool) MZGO_L(prior) MZGO_L(child) MZGO_L(visits) MZGO_L(wsum) MZGO_L(root_prior) MZGO_L(path)
+  MZGO_L(nodes) MZGO_L(nact) MZGO_L(stones) MZGO_L(invd) MZGO_L(meta) MZGO_L(rec_stones) MZGO_L(rec_invd)
+  MZGO_L(rec_flags) MZGO_L(rec_action) MZGO_L(rec_value) MZGO_L(rec_policy) MZGO_L(rec_reward) MZGO_L(game_len)
+  MZGO_L(final_reward) MZGO_L(status) MZGO_L(jobs) MZGO_L(counters) MZGO_L(stamps)
+#undef MZGO_L
+  return r;
+}
 
 template <class G>
 struct TreeViewOf {
@@ -1363,6 +1397,10 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     const int* info = J.info();
     const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3], kind = info[4];
     const NetParams np = select_params(net != 0, np_b, np_a);
+#ifdef MZGO_DIAG_HELPER_SKIP
+    // (diagnostic builds: helpers leave job kinds in the bit mask to the game's workgroup)
+    if ((MZGO_DIAG_HELPER_SKIP >> kind) & 1) continue;
+#endif
     if (kind == 3) {                                   // replay checks of a batch (verify_batch)
       constexpr int DV = verify_depth<G>();
       typedef VerifyLds<G, DV> V;
@@ -2041,8 +2079,8 @@ struct PlayParams {
 };
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np_a, NetParams np_b,
-                                                             SearchParams sp, PlayParams pp, EngineArrays E) {
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_selfplay_move(NetParams np_a_arg, NetParams np_b_arg,
+                                                             SearchParams sp, PlayParams pp, EngineArrays E_arg) {
   typedef Geo<N, C> G;
   __shared__ Smem<G> sm;
   static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
@@ -2055,14 +2093,15 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if ((int)blockIdx.x >= games) {
     if constexpr (Smem<G>::GLOBAL_Y && G::WINO) {
       wino_raw_zero<G>(sm.raw);                          // the conv strips' zero halo
-      helper_loop<G>(sm, np_a, np_b, sp, E, (blockIdx.x - games) % games);
+      helper_loop<G>(sm, np_a_arg, np_b_arg, sp, E_arg, (blockIdx.x - games) % games);
     }
     return;
   }
   const int g = blockIdx.x;
+  const EngineArrays& E = E_arg;
   auto release_helpers = [&]() {
     if (sp.helpers > 0 && threadIdx.x == 0)
-      __hip_atomic_store(job_of<G>(E, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(job_of<G>(E_arg, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   if (E.status[g] != 0) { release_helpers(); return; }
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
@@ -2083,6 +2122,10 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   unsigned long long* tm = nullptr;
 #endif
   const int mv = m.moves;
+  // this move's view of the arguments (launder_global: no address arithmetic
+  // of the move is hoisted above this point)
+  const EngineArrays E = launder_arrays(E_arg);
+  const NetParams np_a = launder_params(np_a_arg), np_b = launder_params(np_b_arg);
   // arena (main.py:535-549): turn 0 = "current" (np_a), 1 = "best" (np_b); game
   // i starts with turn i % 2 (evaluate, :597-599)
   // (field by field: a reference chosen between the two by-value kernel

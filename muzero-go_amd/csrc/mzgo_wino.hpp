@@ -117,6 +117,10 @@ template <class G, int CIN>
 __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const float* my, int quad, int t,
                                                     int e, int ty, int tx) {
   constexpr int S4 = CIN / 32, PW = WinoRaw<G>::PW, RS = WinoRaw<G>::STRIDE;
+  // the last tile column's patch may run past its padded row (19x19: 3 * 7
+  // columns + 2 > 21): into the next row's halo column and first cell, and
+  // for the last row into the junk slot, which every writer leaves 0
+  static_assert((WinoRaw<G>::PH - 1) * PW + 3 * (Wino<G>::TX - 1) + 4 < RS, "patch reads stay in the plane slot");
   const float* s = my + e * RS + (2 * ty) * PW + 3 * tx;   // tile's top-left (padded coords)
   float d[4][5];
 #pragma unroll
@@ -252,7 +256,7 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
       for (int p = 0; p < PER; ++p) {
         const float ec = emb ? eg[k][p] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) my[widx[p][r]] = rg[k][p][r] + ec;
+        for (int r = 0; r < 4; ++r) my[widx[p][r]] = widx[p][r] == R::PLANE ? 0.f : rg[k][p][r] + ec;
       }
       wave_lds_sync();
       if (st && k == 0) st->lap(29);
@@ -289,7 +293,12 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
         const int i = lane + 64 * p;
         const int ee = min(i, NE - 1) / (PH * G::N), r = min(i, NE - 1) - ee * (PH * G::N);
         const int py = r / G::N, x = r - py * G::N;
-        my[i < NE ? ee * RS + py * PW + x + 1 : R::PLANE] = rv[k][p];
+        // (surplus lanes write 0 to the junk slot: at 19x19 the last tile
+        // column's 5-column patch of the last row runs 2 floats past the row
+        // into it, and a value left there by an earlier conv would move that
+        // tile's valid outputs by rounding -- the slot must be the same
+        // whichever conv this workgroup ran before)
+        my[i < NE ? ee * RS + py * PW + x + 1 : R::PLANE] = i < NE ? rv[k][p] : 0.f;
       }
       wave_lds_sync();
       wino_transform_quad<G, CIN>(V, my, quad, t, e, ty, tx);

@@ -75,6 +75,8 @@ SIGNATURES = {
     "mzgo_selfplay_inject_noise": (_I, [_P, _P]),
     "mzgo_records_export": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mzgo_records_pack": (_I, [_P, _P, ctypes.c_int64, _P, _P]),
+    "mzgo_dyn_conv_backward_workspace": (_I, [_I, _I, ctypes.POINTER(ctypes.c_int64)]),
+    "mzgo_dyn_conv_backward": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, ctypes.c_int64, _P]),
 }
 
 

@@ -24,14 +24,16 @@ on the device, every game of a batch at once) and trains on it:
   On the GPU the unroll's forward runs on the HIP kernels
   (``initial_inference_hip`` / ``recurrent_inference_hip``: the engine's
   k_initial_inference / k_recurrent_inference for the 3x3 convs, autograd
-  Functions whose backward is torch's -- from the saved input and output for
-  the dynamics conv, by recomputing the representation's hidden activations);
-  the 1x1 heads stay torch ops on the engine's latents.
+  Functions whose backward is the HIP kernels of csrc/mzgo_train.hip for the
+  dynamics conv -- from the saved input and output -- and torch's for the
+  representation, by recomputing its hidden activations); the 1x1 heads stay
+  torch ops on the engine's latents.
 
 ``initial_inference_torch`` / ``recurrent_inference_torch`` restate
 main.py:72-144 with torch ops on the module's own parameters (reference
 mode, and the CPU).  Replay buffers restate main.py:158-244.
 """
+import ctypes
 import random
 from dataclasses import dataclass
 
@@ -100,12 +102,34 @@ def recurrent_inference_torch(net, latent, action):
 # the same networks with the forward on the HIP engine (SURVEY.md §8(f) 1:
 # "forward only through HIP, backward via torch")
 # ---------------------------------------------------------------------------
+def dyn_conv_backward_hip(g, nxt, latent, action, emb, weight):
+    """The dynamics conv's backward on the HIP kernels (mzgo_dyn_conv_backward,
+    csrc/mzgo_train.hip: fp32 MFMA implicit GEMMs; replaces
+    torch.nn.grad.conv2d_input / conv2d_weight): with gp = g * [nxt > 0],
+    returns (d latent, d weight, d bias) of nxt = relu(conv3x3(latent +
+    emb[action]) + bias), main.py:97-103."""
+    from ._lib import check, lib, ptr, stream_of
+    B, C, N, _ = latent.shape
+    dev = latent.device
+    f = [t.detach().to(dev, torch.float32).contiguous() for t in (g, nxt, latent, emb, weight)]
+    act = action.to(dev, torch.int64).contiguous()
+    ws = ctypes.c_int64()
+    check(lib.mzgo_dyn_conv_backward_workspace(B, C, ctypes.byref(ws)))
+    work = torch.empty(ws.value, dtype=torch.uint8, device=dev)
+    gx = torch.empty_like(f[2])
+    gw = torch.empty_like(f[4])
+    gb = torch.empty(C, device=dev)
+    check(lib.mzgo_dyn_conv_backward(ptr(f[0]), ptr(f[1]), ptr(f[2]), ptr(act), ptr(f[3]), ptr(f[4]), B, C, N,
+                                     ptr(gx), ptr(gw), ptr(gb), ptr(work), ws.value, stream_of(dev)))
+    return gx, gw, gb
+
+
 class _HipDynamicsConv(torch.autograd.Function):
     """x' = relu(conv3x3(latent + emb[a]) + b) (main.py:97-103) with the
-    forward on the engine's k_recurrent_inference; the backward in torch from
-    the saved input and output (ReLU mask = x' > 0; conv2d_input /
-    conv2d_weight; the embedding's gradient = the input gradient summed over
-    the board, added into row a)."""
+    forward on the engine's k_recurrent_inference and the backward on the
+    HIP backward kernels from the saved input and output (ReLU mask = x' > 0;
+    dyn_conv_backward_hip); the embedding's gradient = the input gradient
+    summed over the board, added into row a."""
 
     @staticmethod
     def forward(ctx, latent, action, weight, bias, emb, net):
@@ -116,11 +140,7 @@ class _HipDynamicsConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         latent, action, weight, emb, nxt = ctx.saved_tensors
-        gp = g * (nxt > 0).to(g.dtype)
-        x = latent + emb[action][:, :, None, None]
-        gx = torch.nn.grad.conv2d_input(x.shape, weight, gp, padding=1)
-        gw = torch.nn.grad.conv2d_weight(x, weight.shape, gp, padding=1)
-        gb = gp.sum(dim=(0, 2, 3))
+        gx, gw, gb = dyn_conv_backward_hip(g, nxt, latent, action, emb, weight)
         gemb = torch.zeros_like(emb).index_add_(0, action, gx.sum(dim=(2, 3)))
         return gx, None, gw, gb, gemb, None
 

@@ -6,5 +6,6 @@ cd "$(dirname "$0")/.."
 B=muzero-go_amd/build_${VARIANT:-stamps}
 mkdir -p $B
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result -DMZGO_STAMPS ${EXTRA:-}"
-ls muzero-go_amd/csrc/*.hip | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc $FLAGS -c -o $B/\$(basename {} .hip).o {}"
+KFLAGS="-mllvm -disable-machine-licm -mllvm -disable-machine-sink"   # the megakernels (see __graft_entry__.py)
+ls muzero-go_amd/csrc/*.hip | xargs -P 8 -I{} sh -c "case {} in *mzgo_kernels_n*) K=\"$KFLAGS\";; *) K=;; esac; /opt/rocm/bin/hipcc $FLAGS \$K -c -o $B/\$(basename {} .hip).o {}"
 /opt/rocm/bin/hipcc $FLAGS -shared -o muzero-go_amd/mzgo/libmzgo_${VARIANT:-stamps}.so $B/*.o

@@ -153,3 +153,32 @@ def test_batched_step_hip_forward_equals_torch_forward():
     assert res[True][0] == pytest.approx(res[False][0], rel=1e-5)
     for k in ("value_loss", "policy_loss", "reward_loss"):
         assert res[True][1][k] == pytest.approx(res[False][1][k], rel=1e-5, abs=1e-7)
+
+
+@pytest.mark.parametrize("N,C,B", [(6, 128, 40), (5, 96, 7), (9, 96, 3), (6, 64, 1), (19, 96, 2)])
+def test_dyn_conv_backward_hip_matches_torch(N, C, B):
+    """The dynamics conv's input / weight / bias gradients on the HIP MFMA
+    kernels (mzgo_dyn_conv_backward) against torch.nn.grad.conv2d_input /
+    conv2d_weight on the same saved tensors (the backward main.py:478-482
+    runs through main.py:97-103).  fp32 with a different summation order:
+    |diff| <= 1e-5 + 1e-4 |ref| (gx, summed over 9C terms) and
+    <= 1e-4 + 1e-4 |ref| for gw / gb (summed over B N^2 terms)."""
+    from mzgo.trainer import dyn_conv_backward_hip
+    A = N * N + 1
+    gen = torch.Generator().manual_seed(N * 1000 + C + B)
+    latent = torch.randn(B, C, N, N, generator=gen).relu().cuda()
+    emb = torch.randn(A, C, generator=gen).cuda()
+    w = (torch.randn(C, C, 3, 3, generator=gen) / (3 * C ** 0.5)).cuda()
+    bias = (torch.randn(C, generator=gen) * 0.1).cuda()
+    action = torch.randint(0, A, (B,), generator=gen).cuda()
+    x = latent + emb[action][:, :, None, None]
+    nxt = torch.relu(torch.nn.functional.conv2d(x, w, bias, padding=1))
+    g = torch.randn(B, C, N, N, generator=gen).cuda()
+    gx, gw, gb = dyn_conv_backward_hip(g, nxt, latent, action, emb, w)
+    gp = g * (nxt > 0).float()
+    rx = torch.nn.grad.conv2d_input(x.shape, w, gp, padding=1)
+    rw = torch.nn.grad.conv2d_weight(x, w.shape, gp, padding=1)
+    rb = gp.sum(dim=(0, 2, 3))
+    torch.testing.assert_close(gx, rx, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(gw, rw, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(gb, rb, atol=1e-4, rtol=1e-4)
