@@ -187,11 +187,30 @@ struct Smem<G, true> {
 // One latent conv: src ([CIN][src_stride], global) (+ emb per channel) ->
 // dst ([COUT][dst_stride], cells < out_cells), NH fused 1x1 head partials left
 // in sm.heads().  All threads; returns synchronised.
+// Factored Y of a conv (YM) written to LDS too, as the expansion's copy L.yc
+// (CACHE boards, one strip): yc overlays only the exchange buffer, which is
+// dead when the epilogue stores (wino_conv's YM store loop reads outs).
+template <class G>
+__device__ __forceinline__ float* y_lds_target(Smem<G>& sm) {
+  if constexpr (G::WINO && decltype(sm.u.f)::CACHE && Wino<G>::NSTRIP == 1) {
+    static_assert(sizeof(sm.u.f.yc) <= sizeof(sm.u.x.red), "the LDS Y copy overlays only the exchange buffer");
+    return sm.u.f.yc;
+  } else {
+    return nullptr;
+  }
+}
+// the head weights of the expansion (the rest of load_y, after a conv that
+// left Y in L.yc)
+template <class G>
+__device__ __forceinline__ void load_hw(Smem<G>& sm, const float* head_w) {
+  for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) sm.u.f.hw[i] = head_w[i];
+}
+
 template <class G, int CIN, int COUT, int NH, bool YM = false>
 __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict__ w, const float* __restrict__ b,
                                             const float* src, int src_stride, const float* emb, float* dst,
                                             int dst_stride, int out_cells, const float* head_w,
-                                            Stamp* st = nullptr) {
+                                            Stamp* st = nullptr, float* ylds = nullptr) {
   if constexpr (G::WINO) {
     // row strips (19x19): strip s reads rows s*SROWS-1 .. (s+1)*SROWS of src,
     // so src must not alias dst (representation ping-pongs through scratch)
@@ -199,7 +218,7 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
       wino_input<G, CIN>(sm.u.v, sm.raw, src, src_stride, emb, s, st);
       if (st) st->lap(1);
       wino_conv<G, CIN, COUT, NH, YM>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, w, b, dst, dst_stride,
-                                  out_cells, head_w, s, st);
+                                  out_cells, head_w, s, st, ylds);
     }
     if constexpr (Wino<G>::NSTRIP > 1) __syncthreads();   // hfin complete
   } else {
@@ -216,13 +235,15 @@ __device__ __forceinline__ void latent_conv(Smem<G>& sm, const float* __restrict
 // returns synchronised (strip boards) / with the stores issued (one strip).
 template <class G>
 __device__ __forceinline__ void latent_conv_rebuilt(Smem<G>& sm, const NetParams& np, const float* ypar,
-                                                    const float* ea, float* dst, Stamp* st = nullptr) {
+                                                    const float* ea, float* dst, Stamp* st = nullptr,
+                                                    float* ylds = nullptr, bool par_in_lds = false) {
   if constexpr (G::WINO) {
     for (int s = 0; s < Wino<G>::NSTRIP; ++s) {
-      wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s);
+      // par_in_lds: the parent's Y is L.yc (ylds), read from there
+      wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s, par_in_lds ? ylds : nullptr);
       if (st) st->lap(1);
       wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
-                                        dst, G::CS, G::CS, nullptr, s, st);
+                                        dst, G::CS, G::CS, nullptr, s, st, ylds);
     }
     if constexpr (Wino<G>::NSTRIP > 1) __syncthreads();
   }
@@ -908,11 +929,12 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
       });
     } else {
       latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, pool, G::CS, G::CS,
-                                          nullptr);
+                                          nullptr, nullptr, y_lds_target<G>(sm));
     }
     __syncthreads();
     if (st) st->lap(60);
-    load_y<G>(sm, pool, np.head_w);
+    if (y_lds_target<G>(sm) != nullptr && !shared_jobs<G>(sp)) load_hw<G>(sm, np.head_w);   // (Y in L.yc already)
+    else load_y<G>(sm, pool, np.head_w);
     if (threadIdx.x == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
     __syncthreads();
     if (st) st->lap(61);
@@ -1566,15 +1588,25 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
                            }
                          });
         } else if (G::WINO && leaf != 0) {
-          latent_conv_rebuilt<G>(sm, np, pool + (size_t)T.path(depth - 1) * node_floats,
-                                 np.etab + (size_t)nact[leaf] * 9 * G::C, yleaf, &st);
+          const int par = T.path(depth - 1);
+          latent_conv_rebuilt<G>(sm, np, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
+                                 yleaf, &st, y_lds_target<G>(sm), y_lds_target<G>(sm) != nullptr && yc == par);
         } else {
           latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS,
-                                              G::CS, nullptr, &st);
+                                              G::CS, nullptr, &st, G::WINO ? y_lds_target<G>(sm) : nullptr);
         }
         __syncthreads();                                 // Y stores before the expansion reads them
         st.lap(82);
-        yc = -1;                                         // the conv overwrote the LDS copy
+        // the conv overwrote the union; one-strip Winograd boards got the
+        // leaf's Y into L.yc by the conv itself (only the head weights reload)
+        if (!sj && G::WINO && y_lds_target<G>(sm) != nullptr) {
+          load_hw<G>(sm, np.head_w);
+          if (threadIdx.x == 0) sm.t.ycache = leaf;
+          yc = leaf;
+          __syncthreads();
+        } else {
+          yc = -1;
+        }
         if (threadIdx.x == 0) { st.wave_add(59, 1); ++convs; }   // convs run
       }
       const int nun = sm.t.nunexp;

@@ -326,10 +326,15 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
 // to 4 waves' planes; after a barrier each wave transforms its quad.  The
 // next slab's loads are in flight during the transform.  Values are
 // bit-identical to materialize + wino_input (the same f32 add and select).
+//
+// ylds: the parent's Y is the expansion's LDS copy (L.yc, which V overlays):
+// every slab's Y is read from it into registers first, and the first barrier
+// (before any V store) orders those reads before the transform overwrites it.
+// Typical late in a game: the leaf is a child of the previous batch's leaf.
 template <class G, int CIN>
 __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float* __restrict__ raw,
                                                    const float* __restrict__ ypar, const float* __restrict__ ea,
-                                                   int strip) {
+                                                   int strip, const float* ylds = nullptr) {
   typedef Wino<G> W;
   typedef WinoRaw<G> R;
   constexpr int RS = R::STRIDE, PW = R::PW, PH = R::PH, C4 = CIN / 4;
@@ -344,24 +349,29 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
   const int tt = t < W::T ? t : W::T - 1;
   const int ty = tt / W::TX, tx = tt - ty * W::TX;
   const int row0 = strip * W::SROWS - 1;
-  const f32x4* Y4 = reinterpret_cast<const f32x4*>(ypar);
+  if constexpr (SLABS > 2) ylds = nullptr;                // (slabs past the 2nd would read overwritten LDS)
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(ylds ? ylds : ypar);
   const f32x4* E4 = reinterpret_cast<const f32x4*>(ea);
-  f32x4 yv[R4], ev[R4];
-  auto load = [&](int k) {
+  f32x4 yv[2][R4], ev[2][R4];                           // slabs k and k + 1
+  auto load = [&](int k, f32x4 (&yd)[R4], f32x4 (&ed)[R4]) {
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
       const int i = min((int)threadIdx.x + r * G::THREADS, NI - 1);
       const int cl = i / F4, q4 = i - cl * F4, py = cl / G::N, x = cl - py * G::N, y = row0 + py;
       const bool on = y >= 0 && y < G::N;
       const int ry = y <= 0 ? 0 : (y >= G::N - 1 ? 2 : 1), rx = x == 0 ? 0 : (x == G::N - 1 ? 2 : 1);
-      yv[r] = Y4[(on ? y * G::N + x : 0) * C4 + F4 * k + q4];
-      ev[r] = E4[(ry * 3 + rx) * C4 + F4 * k + q4];
+      yd[r] = Y4[(on ? y * G::N + x : 0) * C4 + F4 * k + q4];
+      ed[r] = E4[(ry * 3 + rx) * C4 + F4 * k + q4];
     }
   };
   __syncthreads();                                      // the previous conv's epilogue is done with LDS
-  load(0);
-#pragma unroll 1
+  load(0, yv[0], ev[0]);
+  // from LDS: slab 1 too, before the first barrier (V overwrites the copy)
+  if (ylds && SLABS > 1) load(1, yv[1], ev[1]);
+#pragma unroll
   for (int k = 0; k < SLABS; ++k) {
+    f32x4 (&yk)[R4] = yv[k & 1];
+    f32x4 (&ek)[R4] = ev[k & 1];
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
       const int i = threadIdx.x + r * G::THREADS;
@@ -371,12 +381,13 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
         float* dst = raw + ((q4 >> 2) * 4) * 4 * RS + (q4 & 3) * RS + py * PW + x + 1;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float v = yv[r][j] + ev[r][j];
+          const float v = yk[r][j] + ek[r][j];
           dst[j * 4 * RS] = on ? (v > 0.f ? v : 0.f) : 0.f;
         }
       }
     }
-    if (k + 1 < SLABS) load(k + 1);
+    // (HBM: the next slab's loads in flight during this slab's transform)
+    if (k + 1 < SLABS && !ylds) load(k + 1, yv[(k + 1) & 1], ev[(k + 1) & 1]);
     __syncthreads();
     wino_transform_quad<G, CIN>(V, raw + wave * 4 * RS, F4 * k + wave, t, e, ty, tx);
     __syncthreads();                                    // planes read before the next slab / V before the GEMM
@@ -407,7 +418,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
                                           const float* __restrict__ upk,
                                           const float* __restrict__ bias, float* __restrict__ out,
                                           int out_stride, int out_cells, const float* __restrict__ head_w,
-                                          int strip = 0, Stamp* st = nullptr) {
+                                          int strip = 0, Stamp* st = nullptr, float* ylds = nullptr) {
   typedef Wino<G> W;
   constexpr int CH = CIN / 2, S4 = CH / 16, MT = COUT / 16, XI = W::XI;
   constexpr int OS = W::OUT_STRIDE;
@@ -453,7 +464,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       if constexpr (2 * MT == G::WAVES)
         if (g > 0 && g % MZGO_WINO_SYNC == 0) __builtin_amdgcn_s_barrier();
 #endif
-#if MZGO_WINO_PRIO
+#if MZGO_WINO_PRIO == 1
       // progress-ordered issue: a wave that is ahead drops its priority, so
       // the SIMD's three waves advance together (oldest-first issue otherwise
       // leaves the youngest wave's two MFMA chains to finish alone)
@@ -461,6 +472,25 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       else if (g == 1) __builtin_amdgcn_s_setprio(2);
       else if (g == 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
+#elif MZGO_WINO_PRIO == 2
+      // static priority by age: the younger waves of a SIMD (4-7, 8-11: the
+      // arbitration losers) ahead of the older ones, for the whole GEMM
+      if (g == 0) {
+        if (wave >= 8) __builtin_amdgcn_s_setprio(2);
+        else if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+      }
+#elif MZGO_WINO_PRIO == 3
+      // progress-ordered over all five groups, ties broken for the younger waves
+      if (g == 0) __builtin_amdgcn_s_setprio(3);
+      else if (g == 2) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+      } else if (g == 3) {
+        if (wave >= 8) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      } else if (g == 4) {
+        __builtin_amdgcn_s_setprio(0);
+      }
 #endif
       f32x4 acc[XG];
 #pragma unroll
@@ -640,6 +670,9 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       const f32x4 v = {outs[(4 * q) * OS + j], outs[(4 * q + 1) * OS + j], outs[(4 * q + 2) * OS + j],
                        outs[(4 * q + 3) * OS + j]};
       reinterpret_cast<f32x4*>(out + (size_t)(c0 + j) * COUT)[q] = v;
+      // (ylds: the same Y also into LDS -- the expansion's copy, over the
+      // exchange buffer, dead by now -- instead of reading it back from HBM)
+      if (ylds) reinterpret_cast<f32x4*>(ylds + (size_t)(c0 + j) * COUT)[q] = v;
     }
   } else if (out != nullptr) {
     if (out_stride == G::CS && out_cells == G::CS) {

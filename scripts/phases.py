@@ -83,6 +83,9 @@ def main():
                  "what": "1 - mean/max of the games' busy cycles: the CU-time the epoch leaves idle while "
                          "its slowest games finish (one game per CU)"},
         "convs_per_game": float(f[:, 59].mean()),
+        # every slot's mean per game (lap slots: thread 0's partition; others:
+        # wave sums / counters, mzgo_common.hpp's map)
+        "slots_mean_per_game": {int(i): round(float(f[:, i].mean())) for i in range(f.shape[1]) if f[:, i].any()},
     }
     # (written under gpurun_out/, which the GPU call merges back; copy it to
     # profiles/<tag>_phases.json and profiles/latest_phases.json, which bench.py reads)

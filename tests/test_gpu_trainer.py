@@ -107,8 +107,9 @@ def test_batched_mode_trains_on_selfplay_output():
 
 def test_hip_forward_autograd_matches_torch():
     """The unroll's HIP forward (k_initial_inference / k_recurrent_inference)
-    with torch backward: outputs and every parameter / input gradient equal
-    the all-torch graph's to fp32-conv tolerance."""
+    with the HIP dynamics-conv backward (mzgo_dyn_conv_backward) and torch's
+    for the rest: outputs and every parameter / input gradient equal the
+    all-torch graph's to fp32-conv tolerance."""
     import mzgo
     from mzgo.trainer import (initial_inference_hip, initial_inference_torch, recurrent_inference_hip,
                               recurrent_inference_torch)
