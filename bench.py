@@ -124,14 +124,14 @@ def pmc_summary(workload, dynamics, moves_per_launch):
     """Per-launch PMC means of k_selfplay_move from rocprofv3 passes of this
     same bench command (scripts/pmc_selfplay.sh -> profiles/<tag>_pmc.json);
     only a profile of the same workload and launch structure counts."""
-    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
-    if not os.path.exists(path):
-        return None
-    p = json.load(open(path))
-    if (p.get("workload") != workload or p.get("dynamics") != dynamics
-            or p.get("moves_per_launch", 1) != moves_per_launch):
-        return None
-    return p
+    import glob
+    for path in [os.path.join(ROOT, "profiles", "latest_pmc.json")] + \
+            sorted(glob.glob(os.path.join(ROOT, "profiles", "latest_pmc_*.json"))):
+        p = json.load(open(path))
+        if (p.get("workload") == workload and p.get("dynamics") == dynamics
+                and p.get("moves_per_launch", 1) == moves_per_launch):
+            return p
+    return None
 
 
 def phases_summary(workload, moves_per_launch):
@@ -169,11 +169,13 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
     mfma_tf = mfma_l / avg_kern_s / 1e12
     CS = (CELLS + 15) // 16 * 16
     if dynamics == "factored":
-        # per simulation the new node's prior (logit) row; per parent conv the
-        # rebuilt latent (written, read) and its Y (written, read); per move the
-        # representation's input and latent and the record
-        hbm_l = (sims_l * A * 4 + convs_l * (2 * C * CS * 4 + 2 * CELLS * C * 4)
-                 + moves_l * ((6 * CELLS + 2 * C * CS) * 4 + 2 * CELLS + A * 8 + 32))
+        # per simulation the new node's prior (logit) row written; per conv its
+        # input read (the parent's Y, or the root latent: the rebuilt latent is
+        # formed inside the input transform, never stored) and its Y written;
+        # per move the representation's three conv outputs (64, 64, C channels)
+        # written and read back, and the record (planes, policy, scalars)
+        hbm_l = (sims_l * A * 4 + convs_l * 2 * CELLS * C * 4
+                 + moves_l * (2 * (128 + C) * CS * 4 + 2 * CELLS + A * 8 + 32))
     else:
         hbm_l = sims_l * (2 * C * CS * 4 + A * 4) + moves_l * ((6 * CELLS + 2 * C * CS) * 4 + A * 8)
     units = {
@@ -182,7 +184,8 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
                  "what": "executed v_mfma_f32_16x16x4_f32 FLOPs (parent convs + representation)"},
         "hbm": {"achieved": hbm_l / avg_kern_s / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                 "frac": hbm_l / avg_kern_s / 1e9 / PEAK_HBM_GBPS, "per_launch": hbm_l,
-                "what": "algorithmic HBM bytes of the factored search (E[a] table L2-resident, not charged)"},
+                "what": "algorithmic HBM bytes of the factored search (E[a] table and weights L2-resident, "
+                        "not charged; a parent's Y read from the LDS copy still charged)"},
     }
     pmc = pmc_summary(workload, dynamics, moves_per_launch)
     traffic = None
