@@ -213,3 +213,42 @@ def test_selfplay_bench_config_matches_oracle(N, G, S, check):
         assert t["root_n"] == r_root.visit_count == S
         assert abs(t["value"] - r_value) < 1e-5, (g, mv, t["value"], r_value)
         assert abs(hists[g].values[mv] - r_value) < 1e-5
+
+
+@pytest.mark.timeout(600)
+def test_refill_streams_equal_one_engine():
+    """bench.py --refill R (the epoch-tail configuration) runs R
+    engines of G slots with game_base r * G, each on its own HIP stream, so
+    their k_selfplay_move launches overlap on the GPU.  Concurrent engines
+    must not interfere (no shared device state between engines), and a
+    game's identity is its global id game_base + slot: engines (base 0, G)
+    and (base G, G) played concurrently must leave byte-identical records to
+    slots [0, G) and [G, 2G) of one engine of 2G slots played alone."""
+    import mzgo
+    N, G, S, epoch = 9, 128, 200, 5
+    net = _net(N)
+    big = mzgo.SelfPlay(net, 2 * G, S, seed=SEED)
+    M = big.max_moves
+    big.reset(epoch=epoch)
+    big.move(M)
+    torch.cuda.synchronize()
+    ref, ra = _records(big.engine)
+    parts = [mzgo.SelfPlay(net, G, S, seed=SEED, game_base=r * G) for r in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    for sp, st in zip(parts, streams):
+        with torch.cuda.stream(st):
+            sp.reset(epoch=epoch)
+            sp.move(M)
+    torch.cuda.synchronize()
+    for r, sp in enumerate(parts):
+        recs, pa = _records(sp.engine)
+        np.testing.assert_array_equal(pa["status"], ra["status"][r * G:(r + 1) * G])
+        np.testing.assert_array_equal(pa["final"].view(np.uint64), ra["final"][r * G:(r + 1) * G].view(np.uint64))
+        for g in range(G):
+            a, b = recs[g], ref[r * G + g]
+            assert a["length"] == b["length"], (r, g)
+            for k in ("stones", "invd", "flags", "action"):
+                np.testing.assert_array_equal(a[k], b[k], err_msg=f"engine {r} game {g} {k}")
+            for k in ("value", "policy", "reward"):
+                np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64),
+                                              err_msg=f"engine {r} game {g} {k}")
