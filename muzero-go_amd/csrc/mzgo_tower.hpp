@@ -129,7 +129,7 @@ struct TapOff { static constexpr int v = (T / 3) * G::W + (T % 3); };
 #ifdef MZGO_TCONV_STAMPS
 // diagnostic build: per-workgroup cycle sums (wave 0): 0 total, 1 prologue,
 // 2 vmcnt waits, 3 barriers, 4 MFMA steps, 5 epilogue, 6 launches
-__device__ unsigned long long g_tstamps[4096][8][8];   // [block][wave][field]
+__device__ unsigned long long g_tstamps[4096][8][16];   // [block][wave][field]; 8 = s_memrealtime ticks (100 MHz)
 #endif
 
 // 16 bytes of an MFMA fragment (one ds_read_b128).  (Two ds_read_b64 with
@@ -159,6 +159,7 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
   STAMP_T(tstart);
 #ifdef MZGO_TCONV_STAMPS
   unsigned long long acc_wait = 0, acc_bar = 0, acc_mfma = 0;
+  const unsigned long long rstart = __builtin_amdgcn_s_memrealtime();
 #endif
   const int CO = a.co_chunks, CC = a.ci_chunks;
   // block -> (board, cout chunk); a board's chunks on one XCD (blocks b, b+8,
@@ -472,9 +473,403 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
 #ifdef MZGO_TCONV_STAMPS
   if (lane == 0 && bid < 4096) {
     const unsigned long long tend = __builtin_amdgcn_s_memtime();
+    const unsigned long long rend = __builtin_amdgcn_s_memrealtime();
     unsigned long long* g = g_tstamps[bid][wave];
+    g[8] += rend - rstart;
     g[0] += tend - tstart; g[1] += tpro - tstart; g[2] += acc_wait; g[3] += acc_bar; g[4] += acc_mfma;
     g[5] += tend - tloop; g[6] += 1;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_tconv_ks: the same conv with the K dimension split across the two waves
+// of a SIMD.  Wave w = (kh, mg), kh = w >> 2, mg = w & 3: waves kh = 0 take
+// channels 0-31 of every (cin chunk, tap) slice, waves kh = 1 channels 32-63,
+// and each wave owns 6 M tiles (96 pixels) x all 64 couts (24 accumulator
+// tiles) instead of 3 x 64.  Per 16x16x32 MFMA a wave reads 0.42 fragments
+// (6 A + 4 B per 24 MFMAs) instead of 0.58 (3 A + 4 B per 12): 30 instead of
+// 42 ds_read_b128 per wave and kernel-row step for the same 72 MFMAs.  The
+// two halves' partial sums meet once in the epilogue's fp32 staging (kh = 0
+// stores, kh = 1 adds), so a cout's sum is (chain over cin 0-31 of every
+// chunk) + (chain over cin 32-63) -- a different fp32 order, nothing else.
+// Same LDS image, DMA pipeline and barriers as k_tconv.
+// ---------------------------------------------------------------------------
+// experiment knobs (A/B builds): MZGO_TCONV_PRIO 1 = s_setprio 1 around every
+// MFMA group, 2 = static priority for waves 4-7; MZGO_TCONV_ABL_NODMA /
+// _NOBAR = timing ablations (wrong results: no DMA after the first step / no
+// step barriers)
+#ifndef MZGO_TCONV_PRIO
+#define MZGO_TCONV_PRIO 0
+#endif
+constexpr int kPrio = MZGO_TCONV_PRIO;
+#ifndef MZGO_TCONV_DMASPREAD
+#define MZGO_TCONV_DMASPREAD 1
+#endif
+constexpr int kDmaSpread = MZGO_TCONV_DMASPREAD;   // > 0: one DMA piece every kDmaSpread MFMA groups
+#ifdef MZGO_TCONV_ABL_NODMA
+constexpr bool kAblNoDma = true;
+#else
+constexpr bool kAblNoDma = false;
+#endif
+#ifdef MZGO_TCONV_ABL_NOBAR
+constexpr bool kAblNoBar = true;
+#else
+constexpr bool kAblNoBar = false;
+#endif
+
+template <int N>
+struct TConvKsGeo {
+  typedef TConvGeo<N, 8> T;
+  static constexpr int MT = (TGeo<N>::TT + 3) / 4;      // tiles per wave (4 M groups)
+#ifdef MZGO_TCONV_KS_ADIST
+  static constexpr int ADIST = MZGO_TCONV_KS_ADIST;
+#else
+  static constexpr int ADIST = 2;      // 1 and 3 spill at N = 19
+#endif
+  static_assert(ADIST >= 1 && ADIST <= 3 * MT, "A prefetch distance");
+  static_assert(8 * MT * 2 * 1024 <= 2 * T::PB + 2 * T::WSLOT, "the epilogue's accumulator exchange fits the patch buffers + ring");
+};
+
+template <int N>
+__global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
+  typedef TGeo<N> G;
+  typedef TConvGeo<N, 8> T;
+  typedef TConvKsGeo<N> K;
+  constexpr int NW = 8, MT = K::MT, AD = K::ADIST, NG = 3 * MT;
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+  STAMP_T(tstart);
+#ifdef MZGO_TCONV_STAMPS
+  unsigned long long acc_wait = 0, acc_bar = 0, acc_mfma = 0;
+  const unsigned long long rstart = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int CO = a.co_chunks, CC = a.ci_chunks;
+  const int bid = blockIdx.x;
+  int b, cg;
+  if (a.nboards % 8 == 0) {
+    const int x = bid & 7, k = bid >> 3;
+    b = x + 8 * (k / CO);
+    cg = k % CO;
+  } else {
+    b = bid / CO;
+    cg = bid % CO;
+  }
+  if (a.active && !a.active[b]) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = wave >> 2, mg = wave & 3;
+  if constexpr (kPrio == 2)
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  char* const patch0 = lds;
+  char* const wring = lds + 2 * T::PB;
+  float* const sbias = reinterpret_cast<float*>(lds + 2 * T::PB + 2 * T::WSLOT);
+  float* const shw = sbias + 64;
+  const bf16* in = a.in + (long long)(a.in_idx ? a.in_idx[b] : b) * a.in_stride;
+  const bf16* wsrc = a.w + (size_t)cg * CC * 9 * 64 * 64;
+  if (tid < 64) {
+    sbias[tid] = a.bias[cg * 64 + tid];
+    if (a.headw)
+      for (int h = 0; h < 3; ++h) shw[h * 64 + tid] = a.headw[h * CO * 64 + cg * 64 + tid];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  auto issue_patch_pieces = [&](int cc, int buf, int k0, int k1) {
+    const char* src = reinterpret_cast<const char*>(in + (size_t)cc * G::P * 64);
+    for (int k = k0; k < k1; ++k) {
+      const int ii = k * NW + wave;
+      if (ii >= T::PPIECES) break;
+      const int off = ii * 1024 + lane * 16;
+      if (off < T::PBYTES) dma16(src + off, lds_addr(patch0 + buf * T::PB + ii * 1024));
+    }
+  };
+  auto issue_w = [&](int s) {
+    const char* src = reinterpret_cast<const char*>(wsrc + (size_t)s * 3 * 64 * 64);
+    char* slot = wring + (s & 1) * T::WSLOT;
+#pragma unroll
+    for (int k = 0; k < T::WPW; ++k) {
+      const int ii = k * NW + wave;
+      dma16(src + ii * 1024 + lane * 16, lds_addr(slot + ii * 1024));
+    }
+  };
+  const int nsteps = 3 * CC;
+  issue_patch_pieces(0, 0, 0, T::NPW);
+  issue_w(0);
+
+  // this wave's half of a 64-channel row: byte 64 * kh of the pixel's 128
+  const int hx = kh * 64;
+  int qb[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int p = tcell<N>((mg * MT + i) * 16 + (lane & 15));
+    qb[i] = p >= 0 ? (p / N) * G::W + (p % N) : 0;
+  }
+  int boff[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int r = n * 16 + (lane & 15);
+    boff[n] = (r * 128 + (((lane >> 4) ^ ((r >> 1) & 7)) << 4)) ^ hx;
+  }
+  f32x4 acc[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto touch_epilogue = [&]() {
+    if (!a.res) return;
+    const char* r = reinterpret_cast<const char*>(a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride +
+                                                  (size_t)cg * G::P * 64);
+    constexpr int L0 = G::W + 1, NL = (G::N - 1) * G::W + G::N;
+    if (tid < NL) dma4(r + (size_t)(L0 + tid) * 128, lds_addr(lds) + (uint32_t)(T::LDS - 256));
+  };
+  STAMP_T(tpro);
+
+  // A wave whose last tile lies past the board (19x19: tile 23 of wave mg = 3)
+  // skips that tile's MFMAs: the chip holds a lower clock under MFMA load,
+  // so a dead tile's MFMAs cost the live ones time.
+  const bool lastdead = __builtin_amdgcn_readfirstlane((mg + 1) * MT > G::TT);
+  for (int cc = 0; cc < CC; ++cc) {
+    const bool nextp = cc + 1 < CC;
+    const char* pbuf = patch0 + (cc & 1) * T::PB;
+    bf16x8 afn[AD];
+    auto frag_a = [&](int kyv, int kx, int i) {
+      const int q = qb[i] + kyv * G::W + kx;
+      return frag_ld(pbuf + ((q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4)) ^ hx));
+    };
+    auto step = [&](auto kyc) {
+      constexpr int ky = decltype(kyc)::value;
+      const int s = cc * 3 + ky;
+      STAMP_T(ts0);
+      int younger = 0;
+      if (ky >= 1 && ky - 1 < 2 && nextp) younger = T::pieces_at(ky - 1, wave);
+      wait_vmcnt_dyn(younger);
+      STAMP_T(ts1);
+      if constexpr (kAblNoBar) {
+      } else if constexpr (ky > 0) {
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(AD) : "memory");
+        __builtin_amdgcn_s_barrier();
+      } else {
+        lds_barrier();
+      }
+      STAMP_T(ts2);
+      auto issue_dma = [&]() {
+        if constexpr (kAblNoDma) if (s > 0) return;
+        if (s + 1 < nsteps) issue_w(s + 1);
+        if (nextp && ky < 2) {
+          constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
+          issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
+        }
+        if (s == nsteps - 1) touch_epilogue();
+      };
+      // DMA piece j of this step (spread over the groups with kDmaSpread):
+      // weight pieces first, then the next chunk's patch pieces (the vmcnt
+      // accounting of the next step counts the patch pieces issued after W(s+1))
+      constexpr int PK0 = ky == 0 ? 0 : (T::NPW + 1) / 2, PK1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
+      constexpr int NPC = ky < 2 ? PK1 - PK0 : 0, NDMA = T::WPW + NPC;
+      auto dma_piece = [&](int j) {
+        if (j < T::WPW) {
+          if (s + 1 < nsteps) {
+            const int ii = j * NW + wave;
+            dma16(reinterpret_cast<const char*>(wsrc + (size_t)(s + 1) * 3 * 64 * 64) + ii * 1024 + lane * 16,
+                  lds_addr(wring + ((s + 1) & 1) * T::WSLOT + ii * 1024));
+          }
+        } else if (nextp) {
+          const int ii = (PK0 + j - T::WPW) * NW + wave;
+          const int off = ii * 1024 + lane * 16;
+          if (ii < T::PPIECES && off < T::PBYTES)
+            dma16(reinterpret_cast<const char*>(in + (size_t)(cc + 1) * G::P * 64) + off,
+                  lds_addr(patch0 + ((cc + 1) & 1) * T::PB + ii * 1024));
+        }
+      };
+      const char* ws = wring + (s & 1) * T::WSLOT;
+      bf16x8 bf[2][4], af[AD + 1];
+      auto load_b = [&](int kx, bf16x8 (&d)[4]) {
+        const char* wt = ws + kx * 64 * 64 * 2;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) d[n] = frag_ld(wt + boff[n]);
+      };
+      auto load_a = [&](auto gc) {
+        constexpr int g = decltype(gc)::value, kx = g / MT, i = g % MT;
+        af[g % (AD + 1)] = frag_a(ky, kx, i);
+      };
+      load_b(0, bf[0]);
+      if constexpr (ky > 0) {
+#pragma unroll
+        for (int g = 0; g < AD; ++g) af[g] = afn[g];
+      } else {
+        static_for<AD>([&](auto gc) { load_a(gc); });
+      }
+      constexpr bool SPREAD = kDmaSpread > 0 && (NDMA - 1) * kDmaSpread < NG;
+      if constexpr (!SPREAD) issue_dma();
+      else if (s == nsteps - 1) touch_epilogue();
+      auto group = [&](auto gc) {
+        constexpr int g = decltype(gc)::value, kx = g / MT, i = g % MT;
+        if constexpr (SPREAD && g % kDmaSpread == 0 && g / kDmaSpread < NDMA) {
+          dma_piece(g / kDmaSpread);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (i == 0 && kx + 1 < 3) load_b(kx + 1, bf[(kx + 1) & 1]);
+        if constexpr (g + AD < NG) load_a(std::integral_constant<int, g + AD>{});
+        constexpr int nrd = (i == 0 && kx + 1 < 3 ? 4 : 0) + (g + AD < NG ? 1 : 0);
+        if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);
+        if constexpr (kPrio == 1) { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_setprio(1); }
+          if (!(i == MT - 1 && lastdead)) {
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kx & 1][n], af[g % (AD + 1)], acc[i][n], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kPrio == 1) { __builtin_amdgcn_s_setprio(0); __builtin_amdgcn_sched_barrier(0); }
+      };
+      static_for<NG>([&](auto gc) { group(gc); });
+      if constexpr (ky < 2) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < AD; ++g) afn[g] = frag_a(ky + 1, g / MT, g % MT);
+      }
+      STAMP_T(ts3);
+#ifdef MZGO_TCONV_STAMPS
+      acc_wait += ts1 - ts0; acc_bar += ts2 - ts1; acc_mfma += ts3 - ts2;
+#endif
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+  }
+  lds_barrier();
+  STAMP_T(tloop);
+
+  // Epilogue straight from the accumulators (no fp32 staging image).  The
+  // MFMAs above put couts on the output rows: lane l of acc[i][n] holds couts
+  // 16n + 4(l >> 4) .. +3 of pixel (l & 15) of tile i.  1. The two K halves
+  // meet: each wave hands its partner (same mg) the n-tiles the partner
+  // finishes (kh = 0 finishes n = 0, 1; kh = 1 n = 2, 3) through LDS, one
+  // ds_write_b128 / ds_read_b128 per tile (a + b == b + a: the sum is the
+  // same whichever wave forms it).  2. v_permlane16_swap of the two kept
+  // n-tiles gives every lane 8 consecutive couts of its pixel -- one 16-byte
+  // piece: bias, E[a] region term, residual, ReLU, bf16, one store.
+  bf16* out = a.out + (long long)(a.out_idx ? a.out_idx[b] : b) * a.out_stride + (size_t)cg * G::P * 64;
+  const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
+                          : nullptr;
+  constexpr int XBYTES = 8 * MT * 2 * 1024;            // exchange area
+  float* const set = reinterpret_cast<float*>(lds + XBYTES);          // E rows [9][64]
+  float* const hxs = set + 9 * 64;                                     // head partials of kh = 1 [4][MT][16][3]
+  static_assert(XBYTES + (9 * 64 + 4 * MT * 16 * 3) * 4 <= 2 * T::PB + 2 * T::WSLOT, "epilogue LDS");
+  const int row = lane >> 4, col = lane & 15;
+  auto finish = [&](auto khc) {                        // kh as a constant: no dynamic register indexing
+    constexpr int KH = decltype(khc)::value, GIVE = KH == 0 ? 2 : 0, KEEP = 2 - GIVE;
+    f32x4* xch = reinterpret_cast<f32x4*>(lds);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) xch[(((mg * 2 + KH) * MT + i) * 2 + nn) * 64 + lane] = acc[i][GIVE + nn];
+    // this lane's piece after the swap and its 8 couts
+    const int pc = 2 * (KEEP + (row & 1)) + (row >> 1), c0 = pc * 8;
+    int qv[MT];
+    bool okv[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int p = tcell<N>((mg * MT + i) * 16 + col);
+      okv[i] = (mg * MT + i) < G::TT && p >= 0;
+      qv[i] = okv[i] ? (p / N + 1) * G::W + (p % N) + 1 : 0;
+    }
+    bf16x8 r8[MT];
+    if (res) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        if (okv[i]) r8[i] = *reinterpret_cast<const bf16x8*>(res + tpix(qv[i], pc));
+    }
+    if (a.etab) {
+      const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
+      for (int k = tid; k < 9 * 64; k += NW * 64) set[k] = eb[(size_t)(k >> 6) * CO * 64 + (k & 63)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) acc[i][KEEP + nn] += xch[(((mg * 2 + (KH ^ 1)) * MT + i) * 2 + nn) * 64 + lane];
+    float bias[8];
+    {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(sbias + c0), b1 = *reinterpret_cast<const f32x4*>(sbias + c0 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bias[e] = b0[e]; bias[e + 4] = b1[e]; }
+    }
+    float hsum[MT][3];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][KEEP][r]),
+                                                         __float_as_uint(acc[i][KEEP + 1][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[r + 4] = __uint_as_float(sw[1]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias[e];
+      if (a.etab) {
+        const int p = tcell<N>((mg * MT + i) * 16 + col);
+        const int y = okv[i] ? p / N : 0, x = okv[i] ? p % N : 0;
+        const int reg = 3 * (y == 0 ? 0 : (y == N - 1 ? 2 : 1)) + (x == 0 ? 0 : (x == N - 1 ? 2 : 1));
+        const f32x4 e0 = *reinterpret_cast<const f32x4*>(set + reg * 64 + c0);
+        const f32x4 e1 = *reinterpret_cast<const f32x4*>(set + reg * 64 + c0 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[e] += e0[e]; v[e + 4] += e1[e]; }
+      }
+      if (res) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)r8[i][e];
+      }
+      bf16x8 o8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o8[e] = (bf16)(v[e] > 0.f ? v[e] : 0.f);
+      if (okv[i]) *reinterpret_cast<bf16x8*>(out + tpix(qv[i], pc)) = o8;
+      if (a.headw) {
+#pragma unroll
+        for (int hh = 0; hh < 3; ++hh) {
+          float sum = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sum += shw[hh * 64 + c0 + e] * (float)o8[e];
+          sum += __shfl_xor(sum, 16);
+          sum += __shfl_xor(sum, 32);
+          hsum[i][hh] = sum;
+        }
+      }
+    }
+    if (a.headw) {
+      // the pixel's sum over this chunk's 64 couts: (kh = 0's 32) + (kh = 1's 32)
+      if constexpr (KH == 1) {
+        if (row == 0)
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int hh = 0; hh < 3; ++hh) hxs[((mg * MT + i) * 16 + col) * 3 + hh] = hsum[i][hh];
+      }
+      __syncthreads();
+      if constexpr (KH == 0) {
+        if (row == 0)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int p = tcell<N>((mg * MT + i) * 16 + col);
+            if (!okv[i]) continue;
+            float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
+#pragma unroll
+            for (int hh = 0; hh < 3; ++hh) hp[hh * G::CS] = hsum[i][hh] + hxs[((mg * MT + i) * 16 + col) * 3 + hh];
+          }
+      }
+    }
+  };
+  if (kh == 0) finish(std::integral_constant<int, 0>{});
+  else finish(std::integral_constant<int, 1>{});
+  STAMP_T(txch);
+#ifdef MZGO_TCONV_STAMPS
+  if (lane == 0 && bid < 4096) {
+    const unsigned long long tend = __builtin_amdgcn_s_memtime();
+    const unsigned long long rend = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* g = g_tstamps[bid][wave];
+    g[8] += rend - rstart;
+    g[0] += tend - tstart; g[1] += tpro - tstart; g[2] += acc_wait; g[3] += acc_bar; g[4] += acc_mfma;
+    g[5] += tend - tloop; g[6] += 1; g[7] += txch - tloop;
   }
 #endif
 }

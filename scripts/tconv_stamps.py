@@ -14,7 +14,7 @@ sp = mzgo.SelfPlay(net, G, S, seed=1234)
 sp.reset()
 sp.move()
 torch.cuda.synchronize()
-out = (ctypes.c_ulonglong * 64)()
+out = (ctypes.c_ulonglong * 128)()
 f = _lib.lib.mzgo_debug_tconv_stamps
 f.argtypes = [ctypes.c_void_p]
 f(out)                       # zero after warmup
@@ -24,8 +24,10 @@ torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 f(out)
 n = out[6]
-names = ["total", "prologue", "vmcnt waits", "barriers", "MFMA steps", "epilogue"]
-print(f"workgroup-launches {n}, move {dt*1e3:.1f} ms  (wave 0; other waves per column)")
+clk = [out[w * 16] / max(out[w * 16 + 8], 1) * 0.1 for w in range(8)]
+names = ["total", "prologue", "vmcnt waits", "barriers", "MFMA steps", "epilogue", "", "epi: exchange"]
+print(f"workgroup-launches {n}, move {dt*1e3:.1f} ms  (wave 0; other waves per column); in-kernel clock GHz per wave: " + " ".join(f"{c:.3f}" for c in clk))
 for k, nm in enumerate(names):
-    per = " ".join(f"{out[w * 8 + k] / max(out[w * 8 + 6], 1):7.0f}" for w in range(8))
+    if not nm: continue
+    per = " ".join(f"{out[w * 16 + k] / max(out[w * 16 + 6], 1):7.0f}" for w in range(8))
     print(f"  {nm:12s} {out[k] / max(n, 1):10.0f} cycles/launch  ({out[k] / max(out[0], 1) * 100:5.1f} %)  waves: {per}")
