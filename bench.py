@@ -237,7 +237,8 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, towers):
     alg = boards * 2 * N * N * 9 * C * C
     exe = boards * 2 * 16 * ((N * N + 15) // 16) * 9 * C * C
     ach = alg / avg_launch_s / 1e12
-    out = {"bound": "mfma", "kernel": f"k_tconv<{N}>", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS,
+    kname = "k_tconv" if os.environ.get("MZGO_TCONV_KS") == "0" else "k_tconv_ks"
+    out = {"bound": "mfma", "kernel": f"{kname}<{N}>", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS,
            "unit": "TFLOP/s", "frac": ach / PEAK_BF16_MFMA_TFLOPS, "traffic": None,
            "avg_launch_ms": avg_launch_s * 1e3, "launches_per_simulation": L, "boards_per_launch": boards,
            "flops_per_launch": alg, "executed_flops_per_launch": exe,
@@ -251,6 +252,17 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, towers):
             out["traffic"] = p.get("hbm_bytes_per_launch")
             out["pmc_source"] = f"profiles/{p['tag']}_pmc.json"
             out["pmc"] = p.get("derived")
+            clk = (p.get("derived") or {}).get("in_kernel_clock_GHz")
+            if clk:
+                # the chip holds ~2.2 GHz under this kernel's bf16 MFMA load:
+                # the fraction of the dense peak at the clock it actually runs
+                out["frac_at_in_kernel_clock"] = ach / (PEAK_BF16_MFMA_TFLOPS * clk / 2.4)
+    pw = os.path.join(ROOT, "profiles", "r3_power_clock.json")
+    if os.path.exists(pw):
+        summ = json.load(open(pw)).get("summary", {})
+        for k, v in summ.items():
+            if k.startswith("config 5"):
+                out["power"] = dict(v, source="profiles/r3_power_clock.json (rocm-smi during the bench; cap 1400 W)")
     return out
 
 

@@ -20,6 +20,7 @@ dynamics = sys.argv[3] if len(sys.argv) > 3 else "factored"
 kernel = sys.argv[4] if len(sys.argv) > 4 else "k_selfplay_move"
 moves_per_launch = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # bench.py --moves-per-launch (0: whole games)
 latest = sys.argv[6] if len(sys.argv) > 6 else "latest_pmc.json"       # the file bench.py reads
+in_clk = float(sys.argv[7]) if len(sys.argv) > 7 else 0.0   # in-kernel clock (GHz) from a stamps build, optional
 src = os.path.join("gpurun_out", f"pmc_{tag}")
 os.makedirs("profiles", exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join("profiles", f"{tag}_kernel_stats.csv"))
@@ -72,6 +73,10 @@ if "GRBM_GUI_ACTIVE" in c:
         "wave_wait_any_share": c.get("SQ_WAIT_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
         "wave_issue_stall_share": c.get("SQ_WAIT_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
         "wave_active_share": c.get("SQ_ACTIVE_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0)),
+        **({"in_kernel_clock_GHz": in_clk,
+            "mfma_busy_frac_at_in_kernel_clock": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (4 * 256 * in_clk * 1e9 * dur),
+            "in_kernel_clock_source": "s_memtime / s_memrealtime deltas of a -DMZGO_TCONV_STAMPS build "
+                                      "(scripts/tconv_stamps.py), same workload"} if in_clk > 0 else {}),
         "note": "fractions of CU-cycles at effective_clock_GHz (see clock_source); "
                 "VALU peak 2 wave-instr/clk/CU, MFMA busy summed over 4 SIMDs, LDS array one cycle/clk/CU; "
                 "wave shares of SQ_WAVE_CYCLES (quad-cycles, as the SQ_WAIT_*/ACTIVE_* counters)",
