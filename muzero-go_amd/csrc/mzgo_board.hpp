@@ -43,10 +43,10 @@ struct BoardLds {
 template <class G>
 struct BoardWG {
   static constexpr int SIZE = G::THREADS;
-  __device__ static int id() { return threadIdx.x; }
+  __device__ static int id() { return tid_local(); }
   __device__ static void sync() { __syncthreads(); }
   __device__ static bool any(int v) { return __syncthreads_or(v) != 0; }
-  __device__ static bool leader() { return threadIdx.x == 0; }
+  __device__ static bool leader() { return tid_local() == 0; }
 };
 template <class G>
 __device__ __forceinline__ bool nbr(int c, int d, int& n) {

@@ -142,6 +142,16 @@ __device__ __forceinline__ int lane_id_local() {
   return l;
 }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// thread index the compiler cannot hoist out of the move / simulation loops
+// (as lane_id_local): IR-level LICM otherwise lifts every phase's
+// threadIdx-derived LDS offsets to the kernel entry, where they stay live
+// across the whole-game loop and spill (k_selfplay_move<9,96>: 236 -> 0 B
+// scratch, 168 -> 160 VGPRs)
+__device__ __forceinline__ int tid_local() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
 
 // Order LDS traffic between lanes of one wave (no workgroup barrier needed).
 __device__ __forceinline__ void wave_lds_sync() {

@@ -49,7 +49,7 @@ __device__ __forceinline__ void stage_board(float* __restrict__ lds, const float
   if (src_stride == G::CS) {
     constexpr int Q = G::CS / 4;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (int i = threadIdx.x; i < nch * Q; i += G::THREADS) {
+    for (int i = tid_local(); i < nch * Q; i += G::THREADS) {
       int c = i / Q, q = i - c * Q;
       float4 v = s4[c * Q + q];
       if (emb) {
@@ -64,13 +64,13 @@ __device__ __forceinline__ void stage_board(float* __restrict__ lds, const float
       *reinterpret_cast<float4*>(lds + c * G::CPAD + q * 4) = v;
     }
   } else {
-    for (int i = threadIdx.x; i < nch * G::CELLS; i += G::THREADS) {
+    for (int i = tid_local(); i < nch * G::CELLS; i += G::THREADS) {
       int c = i / G::CELLS, j = i - c * G::CELLS;
       float v = src[c * src_stride + j];
       if (emb) v += emb[c];
       lds[c * G::CPAD + j] = v;
     }
-    for (int c = threadIdx.x; c < nch; c += G::THREADS) lds[c * G::CPAD + G::CELLS] = 0.f;
+    for (int c = tid_local(); c < nch; c += G::THREADS) lds[c * G::CPAD + G::CELLS] = 0.f;
   }
 }
 
@@ -85,7 +85,7 @@ static_assert(Geo<9, 96>::CELLS < Geo<9, 96>::CS && Geo<19, 96>::CELLS < Geo<19,
 // Zero channels [c0, c1) of an LDS board (input padding of conv1: 6 -> 8 ch).
 template <class G>
 __device__ __forceinline__ void zero_channels(float* lds, int c0, int c1) {
-  for (int i = threadIdx.x; i < (c1 - c0) * G::CPAD; i += G::THREADS) lds[c0 * G::CPAD + i] = 0.f;
+  for (int i = tid_local(); i < (c1 - c0) * G::CPAD; i += G::THREADS) lds[c0 * G::CPAD + i] = 0.f;
 }
 
 // Head accumulation target: hp[cog][h][cell] in LDS, summed in fixed order later.

@@ -116,10 +116,10 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
   const f32x4* W4 = reinterpret_cast<const f32x4*>(hw);
   f32x4* C4 = reinterpret_cast<f32x4*>(lds.yc);
   f32x4* CW = reinterpret_cast<f32x4*>(lds.hw);
-  const int j = threadIdx.x & (X::LPC - 1);
+  const int j = tid_local() & (X::LPC - 1);
 #pragma unroll
   for (int pass = 0; pass < X::PASSES; ++pass) {
-    const int cell = pass * X::CPP + threadIdx.x / X::LPC;
+    const int cell = pass * X::CPP + tid_local() / X::LPC;
     const int cl = cell < G::CELLS ? cell : G::CELLS - 1;
     const int reg = region_of<G>(cl);
     f32x4 y[X::PERL], e[X::PERL];
@@ -162,7 +162,7 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
         wr = CW[c4]; wv = CW[X::C4 + c4]; wp = CW[2 * X::C4 + c4];
       } else {
         wr = W4[c4]; wv = W4[X::C4 + c4]; wp = W4[2 * X::C4 + c4];
-        if (L::CACHE && pass == 0 && threadIdx.x < X::LPC) {   // one writer per weight
+        if (L::CACHE && pass == 0 && tid_local() < X::LPC) {   // one writer per weight
           CW[c4] = wr; CW[X::C4 + c4] = wv; CW[2 * X::C4 + c4] = wp;
         }
       }
@@ -343,7 +343,7 @@ __device__ __forceinline__ void materialize(float* __restrict__ dst, const float
   auto load = [&](int c0) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int i = min((int)threadIdx.x + r * G::THREADS, NI - 1);
+      const int i = min(tid_local() + r * G::THREADS, NI - 1);
       const int p = i / (CB / 4), q = i - p * (CB / 4);
       y[r] = Y4[p * C4 + c0 / 4 + q];
       e[r] = E4[region_of<G>(p) * C4 + c0 / 4 + q];
@@ -353,7 +353,7 @@ __device__ __forceinline__ void materialize(float* __restrict__ dst, const float
   for (int c0 = 0; c0 < G::C; c0 += CB) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int i = threadIdx.x + r * G::THREADS;
+      const int i = tid_local() + r * G::THREADS;
       if (i < NI) {
         const int p = i / (CB / 4), q = i - p * (CB / 4);
 #pragma unroll
@@ -365,7 +365,7 @@ __device__ __forceinline__ void materialize(float* __restrict__ dst, const float
     }
     if (c0 + CB < G::C) load(c0 + CB);
     __syncthreads();
-    for (int i = threadIdx.x; i < CB * G::CS; i += G::THREADS) {
+    for (int i = tid_local(); i < CB * G::CS; i += G::THREADS) {
       const int c = i / G::CS, p = i - c * G::CS;
       dst[(size_t)(c0 + c) * G::CS + p] = p < G::CELLS ? lds[c * CSP + p] : 0.f;
     }

@@ -203,7 +203,7 @@ __device__ __forceinline__ float* y_lds_target(Smem<G>& sm) {
 // left Y in L.yc)
 template <class G>
 __device__ __forceinline__ void load_hw(Smem<G>& sm, const float* head_w) {
-  for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) sm.u.f.hw[i] = head_w[i];
+  for (int i = tid_local(); i < 3 * G::C; i += G::THREADS) sm.u.f.hw[i] = head_w[i];
 }
 
 template <class G, int CIN, int COUT, int NH, bool YM = false>
@@ -284,7 +284,7 @@ __device__ __forceinline__ void representation(Smem<G>& sm, const NetParams& np,
                                       int lat_stride, float* scr, unsigned long long* ts = nullptr,
                                       Jobs jobs = Jobs{}) {
   float* mid = rep_needs_scratch<G>() ? scr : lat;
-  for (int i = threadIdx.x; i < 6 * G::CELLS; i += G::THREADS) {
+  for (int i = tid_local(); i < 6 * G::CELLS; i += G::THREADS) {
     const int c = i / G::CELLS, j = i - c * G::CELLS;
     sm.u.in[c * G::CPAD + j] = planes(c, j);
   }
@@ -341,8 +341,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   float* lat = latent + (size_t)b * G::C * G::CELLS;
   float* scr = scratch ? scratch + (size_t)b * 64 * G::CELLS : nullptr;
   representation<G>(sm, np, [&](int c, int j) { return o[c * G::CELLS + j]; }, lat, G::CELLS, scr);
-  for (int a = threadIdx.x; a < G::A; a += G::THREADS) logits[(size_t)b * G::A + a] = sm.t.logits[a];
-  if (threadIdx.x == 0) value[b] = sm.t.value;
+  for (int a = tid_local(); a < G::A; a += G::THREADS) logits[(size_t)b * G::A + a] = sm.t.logits[a];
+  if (tid_local() == 0) value[b] = sm.t.value;
 }
 
 template <int N, int C>
@@ -357,13 +357,13 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const int b = blockIdx.x;
   int64_t a = action[b];
   if (a < 0 || a >= G::A) {            // nn.Embedding would raise IndexError
-    if (threadIdx.x == 0) atomicOr(err, 1);
+    if (tid_local() == 0) atomicOr(err, 1);
     a = 0;
   }
   dynamics<G>(sm, np, latent + (size_t)b * G::C * G::CELLS, G::CELLS, (int)a,
               next_latent + (size_t)b * G::C * G::CELLS, G::CELLS);
-  for (int i = threadIdx.x; i < G::A; i += G::THREADS) logits[(size_t)b * G::A + i] = sm.t.logits[i];
-  if (threadIdx.x == 0) { reward[b] = sm.t.reward; value[b] = sm.t.value; }
+  for (int i = tid_local(); i < G::A; i += G::THREADS) logits[(size_t)b * G::A + i] = sm.t.logits[i];
+  if (tid_local() == 0) { reward[b] = sm.t.reward; value[b] = sm.t.value; }
 }
 
 // ---------------------------------------------------------------------------
@@ -474,12 +474,12 @@ __device__ __forceinline__ void load_y(Smem<G>& sm, const float* y, const float*
   if constexpr (XL::CACHE) {
     const f32x4* src = reinterpret_cast<const f32x4*>(y);
     f32x4* dst = reinterpret_cast<f32x4*>(L.yc);
-    for (int i = threadIdx.x; i < G::CELLS * G::C / 4; i += G::THREADS) dst[i] = src[i];
+    for (int i = tid_local(); i < G::CELLS * G::C / 4; i += G::THREADS) dst[i] = src[i];
   }
   if constexpr (XL::CACHE || XL::BATCH)
-    for (int i = threadIdx.x; i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
+    for (int i = tid_local(); i < 3 * G::C; i += G::THREADS) L.hw[i] = head_w[i];
   if constexpr (XL::GLOBAL_Y)
-    for (int i = threadIdx.x; i < XL::RPAIRS; i += G::THREADS) L.rpair[i] = ExpandPlan<G>::pair_entry(i >> 3, i & 7);
+    for (int i = tid_local(); i < XL::RPAIRS; i += G::THREADS) L.rpair[i] = ExpandPlan<G>::pair_entry(i >> 3, i & 7);
 }
 
 // ---------------------------------------------------------------------------
@@ -554,7 +554,7 @@ __device__ __forceinline__ bool shared_jobs(const SearchParams& sp) {
 // row the helper read belongs to s, and no stale done add can reach s + 1.
 __device__ __forceinline__ unsigned job_begin(const JobView& J, int total, unsigned first = 0) {
   const unsigned bseq = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     __hip_atomic_store(J.done(), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(J.claim(), (unsigned long long)bseq << 32 | (unsigned)total << 16 | first, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -565,7 +565,7 @@ __device__ __forceinline__ unsigned job_begin(const JobView& J, int total, unsig
 __device__ __forceinline__ void job_publish(const JobView& J, unsigned bseq) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_store(J.seq(), bseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -573,7 +573,7 @@ __device__ __forceinline__ void job_publish(const JobView& J, unsigned bseq) {
 // this workgroup's `mine` units added; wait until all `total` are done
 // (every helper adds after its release), then acquire.  All threads.
 __device__ __forceinline__ void job_wait(const JobView& J, int mine, int total) {
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     unsigned d = __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
     while (d < (unsigned)total) {
       __builtin_amdgcn_s_sleep(4);
@@ -588,7 +588,7 @@ __device__ __forceinline__ void job_wait(const JobView& J, int mine, int total) 
 // claims, the workgroup gets it through LDS.  All threads.
 template <class G>
 __device__ __forceinline__ int job_claim(Smem<G>& sm, const JobView& J, unsigned bseq, int total, int step) {
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     int c0 = -1;
     unsigned long long c = __hip_atomic_load(J.claim(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {                                       // (a failed CAS means another claim succeeded)
@@ -646,7 +646,7 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
                                             Stamp* st = nullptr, int par = -1, int act = 0, Pre pre = Pre{}) {
   const JobView J = job_of<G>(E, g);
   const unsigned bseq = job_begin(J, Wino<G>::NSTRIP);
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     int* info = J.info();
     info[0] = Wino<G>::NSTRIP; info[1] = par; info[2] = leaf; info[3] = net; info[4] = par >= 0 ? 2 : 1;
     info[5] = act;
@@ -692,7 +692,7 @@ __device__ __forceinline__ void rep_shared(Smem<G>& sm, const NetParams& np, con
   float* pool = pool_of<G>(E, g);
   float* lat = pool + (size_t)(E.S + 1) * G::C * G::CS;
   const unsigned bseq = job_begin(J, Wino<G>::NSTRIP);
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     int* info = J.info();
     info[0] = Wino<G>::NSTRIP; info[1] = 0; info[2] = 0; info[3] = net; info[4] = k == 2 ? 4 : 5;
   }
@@ -702,7 +702,7 @@ __device__ __forceinline__ void rep_shared(Smem<G>& sm, const NetParams& np, con
                                                        np.head_w + G::C, J.hfin(G::A));
   job_wait(J, mine, Wino<G>::NSTRIP);
   if (k == 3)
-    for (int i = threadIdx.x; i < 2 * G::CS; i += G::THREADS) sm.hfin[i] = J.hfin(G::A)[i];
+    for (int i = tid_local(); i < 2 * G::CS; i += G::THREADS) sm.hfin[i] = J.hfin(G::A)[i];
   __syncthreads();
   }
 }
@@ -816,8 +816,8 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
   // the job first (geometry, the root's mask, the actions known already:
   // i0 of them), then the picks (pick_all, wave 0; tagged entries: a helper
   // that claims a round before they are out waits for its entry)
-  for (int a = threadIdx.x; a < G::A; a += G::THREADS) J.valid(G::A)[a] = sm.t.valid[a];
-  if (threadIdx.x == 0) {
+  for (int a = tid_local(); a < G::A; a += G::THREADS) J.valid(G::A)[a] = sm.t.valid[a];
+  if (tid_local() == 0) {
     int* info = J.info();
     info[0] = B; info[1] = nid0; info[2] = leaf; info[3] = net; info[4] = 0;
     *J.pass_prior() = sm.t.pass_prior;
@@ -837,12 +837,12 @@ __device__ __forceinline__ void batch_expand_shared(Smem<G>& sm, const NetParams
   const int mine = job_rounds<G, LAZY, !LAZY>(sm, np, sp, TV, yg, J, bseq, B, nid0, prepicked, st);
   if (st) st->lap(42);
   if (prepicked)
-    for (int k = threadIdx.x; k < B; k += G::THREADS)
+    for (int k = tid_local(); k < B; k += G::THREADS)
       L.acts[k] = (int)(unsigned)__hip_atomic_load(J.acts() + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   pre_wait();                                        // (the replay checks' first level rows, verify_preload)
   job_wait(J, mine, B);
   const double* bvg = J.bv(G::A);
-  for (int k = threadIdx.x; k < B; k += G::THREADS) L.bv[k] = bvg[k];
+  for (int k = tid_local(); k < B; k += G::THREADS) L.bv[k] = bvg[k];
   __syncthreads();
   if (st) st->lap(43);
 }
@@ -935,7 +935,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
     if (st) st->lap(60);
     if (y_lds_target<G>(sm) != nullptr && !shared_jobs<G>(sp)) load_hw<G>(sm, np.head_w);   // (Y in L.yc already)
     else load_y<G>(sm, pool, np.head_w);
-    if (threadIdx.x == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
+    if (tid_local() == 0) { sm.t.npick = 0; sm.t.ngrab = 0; }
     __syncthreads();
     if (st) st->lap(61);
     if (shared_jobs<G>(sp)) {
@@ -1097,7 +1097,7 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
   const int lane = lane_id_local();
   const bool alt = sp.variant == 0;
   const double* bv = sm.u.f.bv;
-  if (threadIdx.x < DV * G::AP) (&vl.exactm[0][0])[threadIdx.x] = 0;
+  if (tid_local() < DV * G::AP) (&vl.exactm[0][0])[tid_local()] = 0;
   // ---- 1a. jobs 0..nl-1: level l0 + k's children (one wave each); jobs
   // nl..2nl-1: x's sequential value sums for those levels, and in the first
   // group job 2nl: the root's, on other waves at the same time ----
@@ -1300,7 +1300,7 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   const bool alt = sp.variant == 0;
   const double* bv = sm.u.f.bv;
   // the node at depth d takes the share v (-1)^(D + 1 - d) of a batch child's backup
-  if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
+  if (tid_local() < G::AP) vl.failm[tid_local()] = 0;
   // Levels l0 .. l0 + nl - 1 at a time (every (i, l) check is independent of
   // the others; a failing i is recorded in failm whichever group finds it).
   // With helper workgroups (HBM trees), several groups are a job: each
@@ -1313,12 +1313,12 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
   if (shared) {
     const JobView J = job_of<G>(E, g);
     const unsigned bseq = job_begin(J, ngroups, preloaded ? 1u : 0u);
-    if (threadIdx.x == 0) {
+    if (tid_local() == 0) {
       int* info = J.info();
       info[0] = ngroups; info[1] = nid; info[2] = leaf; info[3] = gs; info[4] = 3;
       info[5] = sm.t.ract; info[6] = D; info[7] = B;
     }
-    if (threadIdx.x < G::AP) __hip_atomic_store(J.failm() + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid_local() < G::AP) __hip_atomic_store(J.failm() + tid_local(), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     job_publish(J, bseq);                          // (J.bv holds the batch's values already)
     int mine = 0;
     if (preloaded) {
@@ -1327,21 +1327,21 @@ __device__ __forceinline__ int verify_batch(Smem<G>& sm, const SearchParams& sp,
     }
     for (int grp; (grp = job_claim(sm, J, bseq, ngroups, 1)) >= 0; ++mine)
       verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, grp * gs, min(gs, D - grp * gs), sm.t.ract, false, st);
-    if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
-      __hip_atomic_fetch_or(J.failm() + threadIdx.x, (unsigned long long)vl.failm[threadIdx.x], __ATOMIC_RELAXED,
+    if (mine > 0 && tid_local() < G::AP && vl.failm[tid_local()])
+      __hip_atomic_fetch_or(J.failm() + tid_local(), (unsigned long long)vl.failm[tid_local()], __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     job_wait(J, mine, ngroups);
-    if (threadIdx.x < G::AP)
-      vl.failm[threadIdx.x] = __hip_atomic_load(J.failm() + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid_local() < G::AP)
+      vl.failm[tid_local()] = __hip_atomic_load(J.failm() + tid_local(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     for (int l0 = 0; l0 < D; l0 += DV)
       verify_levels<G, Acc>(sm, sp, TV, T, nact, D, B, l0, D - l0 < DV ? D - l0 : DV, sm.t.ract, l0 == 0, st,
                             preloaded && l0 == 0);
   }
-  if ((D == 0 || shared) && threadIdx.x == 0) prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
-  if (threadIdx.x == 0) {
+  if ((D == 0 || shared) && tid_local() == 0) prefix_sums<G>(T.ws(0), bv, B, alt && ((D + 1) & 1), vl.wroot);
+  if (tid_local() == 0) {
     int f = B;
 #pragma unroll
     for (int j = G::AP - 1; j >= 0; --j) {
@@ -1401,7 +1401,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
   float* pool = pool_of<G>(E, g);
   unsigned last = 0;
   for (;;) {
-    if (threadIdx.x == 0) {
+    if (tid_local() == 0) {
       unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 26); ++spins) {
         __builtin_amdgcn_s_sleep(8);
@@ -1429,8 +1429,8 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       V& vl = *reinterpret_cast<V*>(&sm.u.f.wv[0]);
       const int ngroups = B, gs = info[3], ract = info[5], D = info[6], nb = info[7];
       const double* bvg = J.bv(G::A);
-      for (int k = threadIdx.x; k < nb; k += G::THREADS) sm.u.f.bv[k] = bvg[k];
-      if (threadIdx.x < G::AP) vl.failm[threadIdx.x] = 0;
+      for (int k = tid_local(); k < nb; k += G::THREADS) sm.u.f.bv[k] = bvg[k];
+      if (tid_local() < G::AP) vl.failm[tid_local()] = 0;
       __syncthreads();
       const TreeAcc<G, false> T(TV, sm.t);
       const int* nact = E.nact + (size_t)g * ((size_t)E.S + 1);
@@ -1438,12 +1438,12 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       for (int grp; (grp = job_claim(sm, J, s, ngroups, 1)) >= 0; ++mine)
         verify_levels<G, TreeAcc<G, false>>(sm, sp, TV, T, nact, D, nb, grp * gs, min(gs, D - grp * gs), ract,
                                             false);
-      if (mine > 0 && threadIdx.x < G::AP && vl.failm[threadIdx.x])
-        __hip_atomic_fetch_or(J.failm() + threadIdx.x, (unsigned long long)vl.failm[threadIdx.x], __ATOMIC_RELAXED,
+      if (mine > 0 && tid_local() < G::AP && vl.failm[tid_local()])
+        __hip_atomic_fetch_or(J.failm() + tid_local(), (unsigned long long)vl.failm[tid_local()], __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0 && mine > 0) {
+      if (tid_local() == 0 && mine > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1457,7 +1457,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
                                                               np.head_w + G::C, J.hfin(G::A));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0 && mine > 0) {
+      if (tid_local() == 0 && mine > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1471,14 +1471,14 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
                                       np.etab + (size_t)act * 9 * G::C);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0 && mine > 0) {
+      if (tid_local() == 0 && mine > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       continue;
     }
-    for (int a = threadIdx.x; a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
-    if (threadIdx.x == 0) sm.t.pass_prior = *J.pass_prior();
+    for (int a = tid_local(); a < G::A; a += G::THREADS) sm.t.valid[a] = J.valid(G::A)[a];
+    if (tid_local() == 0) sm.t.pass_prior = *J.pass_prior();
     stage_head_scalars(np.hs, sm.t.hsc);
     load_y<G>(sm, nullptr, np.head_w);                 // (GLOBAL_Y: the head weights only)
     __syncthreads();
@@ -1486,7 +1486,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     const int mine = job_rounds<G, false, true>(sm, np, sp, TV, yg, J, s, B, nid0, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row and value stores
     __syncthreads();
-    if (threadIdx.x == 0 && mine > 0) {
+    if (tid_local() == 0 && mine > 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1520,7 +1520,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   constexpr bool BATCH = decltype(sm.u.f)::BATCH;
   Acc T(TV, sm.t);
   tree_reset_root<G>(T);
-  if (threadIdx.x == 0) { sm.t.newest = -1; sm.t.newp_node = -1; sm.t.ycache = -1; sm.t.rowc_node = -1; }
+  if (tid_local() == 0) { sm.t.newest = -1; sm.t.newp_node = -1; sm.t.ycache = -1; sm.t.rowc_node = -1; }
   __syncthreads();
 
   int nodes = 1, convs = 0;
@@ -1601,13 +1601,13 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         // leaf's Y into L.yc by the conv itself (only the head weights reload)
         if (!sj && G::WINO && y_lds_target<G>(sm) != nullptr) {
           load_hw<G>(sm, np.head_w);
-          if (threadIdx.x == 0) sm.t.ycache = leaf;
+          if (tid_local() == 0) sm.t.ycache = leaf;
           yc = leaf;
           __syncthreads();
         } else {
           yc = -1;
         }
-        if (threadIdx.x == 0) { st.wave_add(59, 1); ++convs; }   // convs run
+        if (tid_local() == 0) { st.wave_add(59, 1); ++convs; }   // convs run
       }
       const int nun = sm.t.nunexp;
       const int B = BATCH ? (nun < S - sim ? nun : S - sim) : 1;
@@ -1617,15 +1617,15 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         if (yc != leaf) load_y<G>(sm, yleaf, np.head_w);
         if constexpr (Acc::LDS) {
           if (leaf != 0 && sm.t.rowc_node != leaf) {      // the replay's selects read leaf's rows from LDS
-            for (int i = threadIdx.x; i < G::A; i += G::THREADS) {
+            for (int i = tid_local(); i < G::A; i += G::THREADS) {
               sm.t.rowc_child[i] = TV.child[(size_t)leaf * G::A + i];
               sm.t.rowc_prior[i] = TV.prior[(size_t)leaf * G::A + i];
             }
             __syncthreads();
-            if (threadIdx.x == 0) sm.t.rowc_node = leaf;
+            if (tid_local() == 0) sm.t.rowc_node = leaf;
           }
         }
-        if (threadIdx.x == 0) { sm.u.f.acts[0] = a; sm.t.npick = 1; sm.t.ngrab = 0; }
+        if (tid_local() == 0) { sm.u.f.acts[0] = a; sm.t.npick = 1; sm.t.ngrab = 0; }
         __syncthreads();
         st.lap(70);
         uint64_t um[G::AP];
@@ -1661,7 +1661,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           nodes += m;
           sim += m;
           st.lap(63);
-          if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
+          if (tid_local() == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
           continue;
         }
         if (wave_id() == 0) {
@@ -1702,19 +1702,19 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         sim += m;
         pending = m < B;
         st.lap(63);
-        if (threadIdx.x == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
+        if (tid_local() == 0) { st.wave_add(31, 1); st.wave_add(28, (unsigned long long)m); }
         continue;
       }
       // ---- one expansion ----
-      if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
+      if (tid_local() == 0) { T.init(nid); sm.t.newest = nid; }
       const unsigned long long t_x = st.now();
       expand_heads<G>(sm.u.f, yleaf, yc == leaf, np.etab + (size_t)a * 9 * G::C, np.head_w);
-      if (threadIdx.x == 0) st.wave_add(56, st.now() - t_x);
+      if (tid_local() == 0) st.wave_add(56, st.now() - t_x);
       __syncthreads();
-      if (threadIdx.x == 0 && decltype(sm.u.f)::CACHE) sm.t.ycache = leaf;   // read by all before the barrier
+      if (tid_local() == 0 && decltype(sm.u.f)::CACHE) sm.t.ycache = leaf;   // read by all before the barrier
       heads = sm.u.f.xh;
     } else {
-      if (threadIdx.x == 0) { T.init(nid); sm.t.newest = nid; }
+      if (tid_local() == 0) { T.init(nid); sm.t.newest = nid; }
       latent_conv<G, G::C, G::C, 3>(sm, np.w_dyn, np.b_dyn, pool + (size_t)leaf * node_floats, G::CS,
                                     np.emb + (size_t)a * G::C, pool + (size_t)nid * node_floats, G::CS, G::CS,
                                     np.head_w, &st);
@@ -1752,7 +1752,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   __syncthreads();
   st.flush();
   tree_flush<G>(T, nodes);
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     E.nodes[g] = nodes;
     // direct dynamics: one conv per expansion
     atomicAdd(&E.counters[3], (unsigned long long)(factored ? convs : nodes - 1));
@@ -1765,7 +1765,7 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
                                   const EngineArrays& E, int g, PlaneFn planes, const double* noise,
                                   uint64_t key, unsigned long long* ts = nullptr) {
   const TreeView TV = TreeViewOf<G>::make(E, g);
-  if (threadIdx.x == 0) sm.t.ngrab = 0;             // draw_dirichlet's counter (build_mask's barrier orders it)
+  if (tid_local() == 0) sm.t.ngrab = 0;             // draw_dirichlet's counter (build_mask's barrier orders it)
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
   float* pool = pool_of<G>(E, g);
   const size_t node_floats = (size_t)G::C * G::CS;
@@ -1805,11 +1805,11 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
 template <class G>
 __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int* out_visits, double* out_value) {
   const TreeView T = TreeViewOf<G>::make(E, g);
-  for (int a = threadIdx.x; a < G::A; a += G::THREADS) {
+  for (int a = tid_local(); a < G::A; a += G::THREADS) {
     const int c = T.child[a];
     if (out_visits) out_visits[(size_t)g * G::A + a] = c >= 0 ? T.visits[c] : 0;
   }
-  if (threadIdx.x == 0 && out_value) {
+  if (tid_local() == 0 && out_value) {
     const int n = T.visits[0];
     out_value[g] = n > 0 ? T.wsum[0] / (double)n : 0.0;
   }
@@ -1856,7 +1856,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 // ---------------------------------------------------------------------------
 template <class G>
 __device__ __forceinline__ void load_board(Smem<G>& sm, const EngineArrays& E, int g, BoardMeta& m) {
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = tid_local(); c < G::CELLS; c += G::THREADS) {
     sm.stone[c] = E.stones[(size_t)g * G::CELLS + c];
     sm.invd[c] = E.invd[(size_t)g * G::CELLS + c];
   }
@@ -1867,11 +1867,11 @@ __device__ __forceinline__ void load_board(Smem<G>& sm, const EngineArrays& E, i
 
 template <class G>
 __device__ __forceinline__ void store_board(Smem<G>& sm, const EngineArrays& E, int g, const BoardMeta& m) {
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = tid_local(); c < G::CELLS; c += G::THREADS) {
     E.stones[(size_t)g * G::CELLS + c] = sm.stone[c];
     E.invd[(size_t)g * G::CELLS + c] = sm.invd[c];
   }
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     int* mm = E.meta + g * 4;
     mm[0] = m.turn; mm[1] = m.passed; mm[2] = m.done; mm[3] = m.moves;
   }
@@ -1893,12 +1893,12 @@ template <int N, int C>
 __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_board_reset(EngineArrays E) {
   typedef Geo<N, C> G;
   const int g = blockIdx.x;
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = tid_local(); c < G::CELLS; c += G::THREADS) {
     E.stones[(size_t)g * G::CELLS + c] = 0;
     E.invd[(size_t)g * G::CELLS + c] = 0;
   }
-  if (threadIdx.x < 4) E.meta[g * 4 + threadIdx.x] = 0;
-  if (threadIdx.x == 0) { E.status[g] = 0; E.game_len[g] = 0; E.final_reward[g] = 0.0; }
+  if (tid_local() < 4) E.meta[g * 4 + tid_local()] = 0;
+  if (tid_local() == 0) { E.status[g] = 0; E.game_len[g] = 0; E.final_reward[g] = 0.0; }
 }
 
 // Step every slot with actions[g] >= 0 (gogame.next_state); status[g] gets a
@@ -1920,7 +1920,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if (st == BOARD_OK) store_board<G>(sm, E, g, m);
   double w = 0.0;
   if (st == BOARD_OK && m.done) w = board_winning<G>(b, komi);
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     if (status) status[g] = st;
     if (winner) winner[g] = w;
   }
@@ -1933,7 +1933,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const int g = blockIdx.x;
   const int* mm = E.meta + g * 4;
   double* p = planes + (size_t)g * 6 * G::CELLS;
-  for (int j = threadIdx.x; j < G::CELLS; j += G::THREADS) {
+  for (int j = tid_local(); j < G::CELLS; j += G::THREADS) {
     const int s = E.stones[(size_t)g * G::CELLS + j];
     p[j] = s == 1; p[G::CELLS + j] = s == 2; p[2 * G::CELLS + j] = mm[0];
     p[3 * G::CELLS + j] = E.invd[(size_t)g * G::CELLS + j];
@@ -2132,7 +2132,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const int g = blockIdx.x;
   const EngineArrays& E = E_arg;
   auto release_helpers = [&]() {
-    if (sp.helpers > 0 && threadIdx.x == 0)
+    if (sp.helpers > 0 && tid_local() == 0)
       __hip_atomic_store(job_of<G>(E_arg, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   if (E.status[g] != 0) { release_helpers(); return; }
@@ -2164,11 +2164,11 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   // arguments would copy both to scratch)
   const NetParams np = select_params(pp.arena && (((pp.game_base + g) + mv) & 1), np_b, np_a);
   const size_t rec = (size_t)g * E.max_moves + mv;
-  for (int c = threadIdx.x; c < G::CELLS; c += G::THREADS) {
+  for (int c = tid_local(); c < G::CELLS; c += G::THREADS) {
     E.rec_stones[rec * G::CELLS + c] = sm.stone[c];
     E.rec_invd[rec * G::CELLS + c] = sm.invd[c];
   }
-  if (threadIdx.x == 0) E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
+  if (tid_local() == 0) E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
 
   const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
   const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
@@ -2208,7 +2208,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #ifdef MZGO_STAMPS
   // move phases (slots 83-87): board load + record, representation, root
   // priors, the simulations, action choice + board step
-  if (threadIdx.x == 0 && E.stamps) {
+  if (tid_local() == 0 && E.stamps) {
     const unsigned long long t5 = __builtin_amdgcn_s_memtime();
     unsigned long long* sl = E.stamps + (size_t)blockIdx.x * kStampPhases;
     sl[83] += tm[1] - tm[0];
@@ -2222,7 +2222,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   }
 #endif
   const bool over = st != BOARD_OK || m.done || m.moves >= E.max_moves;
-  if (threadIdx.x == 0) {
+  if (tid_local() == 0) {
     E.rec_reward[rec] = w;
     atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);
     atomicAdd(&E.counters[1], 1ull);

@@ -151,13 +151,13 @@ __device__ __forceinline__ double mask_of(const TreeLds<G>& t, int a) {
 template <class G, class InvdFn>
 __device__ __forceinline__ void build_mask(TreeLds<G>& t, double pass_epsilon, InvdFn invd) {
   int any = 0;
-  for (int a = threadIdx.x; a < G::A; a += G::THREADS) {
+  for (int a = tid_local(); a < G::A; a += G::THREADS) {
     uint8_t v = a < G::CELLS ? (invd(a) == 0 ? 1 : 0) : 1;
     t.valid[a] = v;
     any |= (a < G::CELLS) && v;
   }
   any = __syncthreads_or(any);
-  if (threadIdx.x == 0) t.pass_prior = any ? pass_epsilon : 1.0;
+  if (tid_local() == 0) t.pass_prior = any ? pass_epsilon : 1.0;
   __syncthreads();
 }
 
@@ -220,7 +220,7 @@ enum : int { HS_RB = 0, HS_FC1W = 1, HS_FC1B = 17, HS_FC2W = 33, HS_FC2B = 49, H
 
 // All threads; visible after the caller's next barrier.
 __device__ __forceinline__ void stage_head_scalars(const HeadScalars& hs, float* dst) {
-  const int i = threadIdx.x;
+  const int i = tid_local();
   if (i >= HS_COUNT) return;
   const float* src;
   if (i == HS_RB) src = hs.reward_b;
@@ -980,17 +980,17 @@ __device__ __forceinline__ void backup(Acc& T, int depth, int nid, double v, boo
 // Reset a tree to a bare root (children unexpanded, stats zero).  All threads.
 template <class G, class Acc>
 __device__ __forceinline__ void tree_reset_root(Acc& T) {
-  for (int a = threadIdx.x; a < G::A; a += G::THREADS) T.set_child(0, a, -1);
+  for (int a = tid_local(); a < G::A; a += G::THREADS) T.set_child(0, a, -1);
   if constexpr (G::TREE_CAP > 0)
-    for (int i = threadIdx.x; i < (G::TREE_CAP + 31) / 32; i += G::THREADS) T.t.rawp[i] = 0u;
-  if (threadIdx.x == 0) { T.init(0); T.set_path(0, 0); }
+    for (int i = tid_local(); i < (G::TREE_CAP + 31) / 32; i += G::THREADS) T.t.rawp[i] = 0u;
+  if (tid_local() == 0) { T.init(0); T.set_path(0, 0); }
 }
 
 // Write LDS-resident stats of nodes [0, nodes) back to HBM.  All threads.
 template <class G, class Acc>
 __device__ __forceinline__ void tree_flush(Acc& T, int nodes) {
   if constexpr (Acc::LDS) {
-    for (int n = threadIdx.x; n < nodes; n += G::THREADS) {
+    for (int n = tid_local(); n < nodes; n += G::THREADS) {
       T.T.visits[n] = T.t.svis[n];
       T.T.wsum[n] = T.t.sws[n];
     }

@@ -181,7 +181,7 @@ __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const
 // All threads; synchronises.
 template <class G>
 __device__ __forceinline__ void wino_raw_zero(float* raw) {
-  for (int i = threadIdx.x; i < WinoRaw<G>::FLOATS; i += G::THREADS) raw[i] = 0.f;
+  for (int i = tid_local(); i < WinoRaw<G>::FLOATS; i += G::THREADS) raw[i] = 0.f;
   __syncthreads();
 }
 
@@ -356,7 +356,7 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
   auto load = [&](int k, f32x4 (&yd)[R4], f32x4 (&ed)[R4]) {
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
-      const int i = min((int)threadIdx.x + r * G::THREADS, NI - 1);
+      const int i = min(tid_local() + r * G::THREADS, NI - 1);
       const int cl = i / F4, q4 = i - cl * F4, py = cl / G::N, x = cl - py * G::N, y = row0 + py;
       const bool on = y >= 0 && y < G::N;
       const int ry = y <= 0 ? 0 : (y >= G::N - 1 ? 2 : 1), rx = x == 0 ? 0 : (x == G::N - 1 ? 2 : 1);
@@ -374,7 +374,7 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
     f32x4 (&ek)[R4] = ev[k & 1];
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
-      const int i = threadIdx.x + r * G::THREADS;
+      const int i = tid_local() + r * G::THREADS;
       if (i < NI) {
         const int cl = i / F4, q4 = i - cl * F4, py = cl / G::N, x = cl - py * G::N, y = row0 + py;
         const bool on = y >= 0 && y < G::N;
@@ -640,7 +640,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   // pad cells of the staged rows are 0 (the pooled layout keeps them 0)
   const bool last = strip == W::NSTRIP - 1;
   if (last)
-    for (int i = threadIdx.x; i < COUT * (G::CS - G::CELLS); i += G::THREADS) {
+    for (int i = tid_local(); i < COUT * (G::CS - G::CELLS); i += G::THREADS) {
       const int co = i / (G::CS - G::CELLS);
       outs[co * OS + G::CELLS - c0 + (i - co * (G::CS - G::CELLS))] = 0.f;
     }
@@ -649,7 +649,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     // strip boards: this strip's head sums over the cout tiles, in a fixed
     // order, into the board-wide hfin [3][CS] (hp is reused by the next strip)
     constexpr int SC = W::SCELLS;
-    for (int i = threadIdx.x; i < NH * SC; i += G::THREADS) {
+    for (int i = tid_local(); i < NH * SC; i += G::THREADS) {
       const int hh = i / SC, lc = i - hh * SC;
       if (c0 + lc < G::CELLS) {
         float v = hp[hh * W::HS + lc];
@@ -665,7 +665,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     // as contiguous float4s): float4 of 4 couts per (cell, cout quad)
     constexpr int Q = COUT / 4;
     const int n = min(c0 + W::SCELLS, G::CELLS) - c0;
-    for (int i = threadIdx.x; i < n * Q; i += G::THREADS) {
+    for (int i = tid_local(); i < n * Q; i += G::THREADS) {
       const int j = i / Q, q = i - j * Q;
       const f32x4 v = {outs[(4 * q) * OS + j], outs[(4 * q + 1) * OS + j], outs[(4 * q + 2) * OS + j],
                        outs[(4 * q + 3) * OS + j]};
@@ -677,7 +677,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   } else if (out != nullptr) {
     if (out_stride == G::CS && out_cells == G::CS) {
       const int Q = ((last ? G::CS : c0 + W::SCELLS) - c0) / 4;   // float4 of this strip's row span
-      for (int i = threadIdx.x; i < COUT * Q; i += G::THREADS) {
+      for (int i = tid_local(); i < COUT * Q; i += G::THREADS) {
         const int co = i / Q, q = i - co * Q;
         const f32x4 v = *reinterpret_cast<const f32x4*>(outs + co * OS + q * 4);
         f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)co * G::CS + c0) + q;
@@ -689,7 +689,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       }
     } else {
       const int n = min(c0 + W::SCELLS, out_cells) - c0;
-      for (int i = threadIdx.x; i < COUT * n; i += G::THREADS) {
+      for (int i = tid_local(); i < COUT * n; i += G::THREADS) {
         const int co = i / n, j = i - co * n;
         out[(size_t)co * out_stride + c0 + j] = outs[co * OS + j];
       }
