@@ -108,7 +108,14 @@ struct WinoRaw {
   // 19x19 (42*ty + 3*tx)
   static constexpr int STRIDE = PLANE + ((11 - PLANE % 32) % 32 + 32) % 32;
   static_assert(STRIDE > PLANE, "a junk slot past each plane");
-  static constexpr int FLOATS = G::WAVES * 4 * STRIDE;   // all waves' slices
+  // wino_input_rebuilt's scatter stores, per ds_write_b32, the 12 channel
+  // quads of ~3 cells into the planes of waves j, j + 4, j + 8: waves j and
+  // j + 8 sit 32 * STRIDE apart, on the same banks, so their slices are
+  // skewed by 8 floats (simulated over both boards: 3.9-way -> 2-way
+  // conflicts; 2-way is the floor at STRIDE = 11 mod 32)
+  static constexpr int SKEW = 8;
+  __device__ static constexpr int base(int wave) { return wave * 4 * STRIDE + ((wave >> 2) == 2 ? SKEW : 0); }
+  static constexpr int FLOATS = G::WAVES * 4 * STRIDE + SKEW;   // all waves' slices
 };
 
 // The 4 x 5 patch of tile (ty, tx) of channel e (plane my + e*RS) -> the 20
@@ -210,7 +217,7 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
   const int tt = t < W::T ? t : W::T - 1;     // pad column: any valid tile (output unused)
   const int ty = tt / W::TX, tx = tt - ty * W::TX;
   const int row0 = strip * W::SROWS - 1;      // board row of padded row 0
-  float* my = raw + wave * 4 * RS;
+  float* my = raw + R::base(wave);
   auto chan = [&](int quad, int ee) {         // channel of quad member ee
     const int h = quad / (S4 * 4), s4 = (quad / 4) % S4, kq = quad % 4;
     return h * CH + 4 * (4 * s4 + ee) + kq;
@@ -378,7 +385,7 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
       if (i < NI) {
         const int cl = i / F4, q4 = i - cl * F4, py = cl / G::N, x = cl - py * G::N, y = row0 + py;
         const bool on = y >= 0 && y < G::N;
-        float* dst = raw + ((q4 >> 2) * 4) * 4 * RS + (q4 & 3) * RS + py * PW + x + 1;
+        float* dst = raw + R::base((q4 >> 2) * 4) + (q4 & 3) * RS + py * PW + x + 1;   // (+ j * 4 * RS: the same skew)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float v = yk[r][j] + ek[r][j];
@@ -389,7 +396,7 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
     // (HBM: the next slab's loads in flight during this slab's transform)
     if (k + 1 < SLABS && !ylds) load(k + 1, yv[(k + 1) & 1], ev[(k + 1) & 1]);
     __syncthreads();
-    wino_transform_quad<G, CIN>(V, raw + wave * 4 * RS, F4 * k + wave, t, e, ty, tx);
+    wino_transform_quad<G, CIN>(V, raw + R::base(wave), F4 * k + wave, t, e, ty, tx);
     __syncthreads();                                    // planes read before the next slab / V before the GEMM
   }
 }
