@@ -113,7 +113,11 @@ struct WinoRaw {
   // j + 8 sit 32 * STRIDE apart, on the same banks, so their slices are
   // skewed by 8 floats (simulated over both boards: 3.9-way -> 2-way
   // conflicts; 2-way is the floor at STRIDE = 11 mod 32)
+#ifdef MZGO_STAMPS
+  static constexpr int SKEW = G::N == 19 ? 0 : 8;   // (the 19x19 stamps build has no 32 B of LDS to spare)
+#else
   static constexpr int SKEW = 8;
+#endif
   __device__ static constexpr int base(int wave) { return wave * 4 * STRIDE + ((wave >> 2) == 2 ? SKEW : 0); }
   static constexpr int FLOATS = G::WAVES * 4 * STRIDE + SKEW;   // all waves' slices
 };
