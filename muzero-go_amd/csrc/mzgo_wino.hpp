@@ -597,16 +597,45 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     ymine[ox] = h == 0 ? yp[ox] : yp[3 + ox];
     ygive[ox] = h == 0 ? yp[3 + ox] : yp[ox];
   }
+  // (one ds_write_b128 / ds_read_b128 per output column: [m][h][ox][lane] f32x4)
+  f32x4* red4 = reinterpret_cast<f32x4*>(red);
   if (active) {
 #pragma unroll
-    for (int ox = 0; ox < 3; ++ox)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        red[((m * 2 + h) * 12 + ox * 4 + r) * 64 + lane] = ygive[ox][r];
+    for (int ox = 0; ox < 3; ++ox) red4[((m * 2 + h) * 3 + ox) * 64 + lane] = ygive[ox];
   }
   __syncthreads();
   if (st) st->lap(7);
   const int c0 = strip * W::SCELLS;          // first cell of this strip
+  if constexpr (YM && NH == 0 && W::NSTRIP == 1) {
+    // The pre-activation Y of a parent conv, cell-major [CELLS][COUT]: lane
+    // (t, kq) holds couts m*16 + 4kq .. +3 of its cells (2ty + h, 3tx + ox),
+    // one float4 of Y each -- stored straight from the registers, no staging
+    // (the LDS copy ylds overlays red: written after every wave's red reads)
+    f32x4 yv[3];
+    int cl[3];
+    bool ok[3];
+    const int ty = t / W::TX, tx = t - ty * W::TX, y = 2 * ty + h;
+#pragma unroll
+    for (int ox = 0; ox < 3; ++ox) {
+      const int x = 3 * tx + ox;
+      ok[ox] = active && t < W::T && y < G::N && x < G::N;
+      cl[ox] = y * G::N + x;
+      if (active) {
+        const f32x4 other = red4[((m * 2 + (1 - h)) * 3 + ox) * 64 + lane];
+        const f32x4 mine = ymine[ox];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) yv[ox][r] = (h == 0 ? mine[r] + other[r] : other[r] + mine[r]) + bb[r];   // (xi half 0) + (xi half 1)
+        if (ok[ox]) reinterpret_cast<f32x4*>(out + (size_t)cl[ox] * COUT)[m * 4 + kq] = yv[ox];
+      }
+    }
+    if (ylds) {
+      __syncthreads();
+#pragma unroll
+      for (int ox = 0; ox < 3; ++ox)
+        if (ok[ox]) reinterpret_cast<f32x4*>(ylds + (size_t)cl[ox] * COUT)[m * 4 + kq] = yv[ox];
+    }
+    return;                                   // (the caller synchronises before reading Y)
+  }
   if (active) {
     const int oy = h;
     const int ty = t / W::TX, tx = t - ty * W::TX;
@@ -623,7 +652,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       const int cell = y * G::N + x;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float other = red[((m * 2 + (1 - h)) * 12 + ox * 4 + r) * 64 + lane];
+        const float other = red4[((m * 2 + (1 - h)) * 3 + ox) * 64 + lane][r];
         const float mine = ymine[ox][r];
         // fixed order: (xi half 0) + (xi half 1)
         float v = (h == 0 ? mine + other : other + mine) + bb[r];
