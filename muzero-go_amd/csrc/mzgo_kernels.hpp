@@ -1561,6 +1561,9 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       float* yleaf = pool + (size_t)leaf * node_floats;
       int yc = sm.t.ycache;
       bool prepicked = false;                            // the batch's picks went out during the conv job
+      static_assert(!decltype(sm.u.f)::CACHE || 3 * G::C <= G::THREADS, "one head weight per thread");
+      float hwpre = 0.f;                                 // this thread's head weight, fetched before the conv
+      bool hwready = false;
       if (!sm.t.yready) {
         const bool sj = shared_jobs<G>(sp);
         // Winograd boards rebuild the latent inside the conv's input
@@ -1589,8 +1592,13 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
                          });
         } else if (G::WINO && leaf != 0) {
           const int par = T.path(depth - 1);
+          // the expansion's head weights (L.hw, which the conv overwrites) are
+          // fetched before the conv and stored after it: the L2 round trip
+          // runs under the conv instead of after it
+          if constexpr (decltype(sm.u.f)::CACHE) hwpre = tid_local() < 3 * G::C ? np.head_w[tid_local()] : 0.f;
           latent_conv_rebuilt<G>(sm, np, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
                                  yleaf, &st, y_lds_target<G>(sm), y_lds_target<G>(sm) != nullptr && yc == par);
+          hwready = true;
         } else {
           latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS,
                                               G::CS, nullptr, &st, G::WINO ? y_lds_target<G>(sm) : nullptr);
@@ -1600,7 +1608,11 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         // the conv overwrote the union; one-strip Winograd boards got the
         // leaf's Y into L.yc by the conv itself (only the head weights reload)
         if (!sj && G::WINO && y_lds_target<G>(sm) != nullptr) {
-          load_hw<G>(sm, np.head_w);
+          if (hwready) {
+            if (tid_local() < 3 * G::C) sm.u.f.hw[tid_local()] = hwpre;
+          } else {
+            load_hw<G>(sm, np.head_w);
+          }
           if (tid_local() == 0) sm.t.ycache = leaf;
           yc = leaf;
           __syncthreads();

@@ -1,5 +1,5 @@
 #!/bin/bash
-# parent-conv Y stored from the registers: GPU suite, then 9x9 A/B against the previous build
+# A/B of the current change: GPU suite, then 9x9 A/B against the previous build
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
