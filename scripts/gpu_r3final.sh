@@ -5,9 +5,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash scripts/pmc_selfplay.sh r3p > gpurun_out/pmc_r3p.log 2>&1 || { tail -20 gpurun_out/pmc_r3p.log; exit 1; }
+bash scripts/pmc_selfplay.sh r3q > gpurun_out/pmc_r3q.log 2>&1 || { tail -20 gpurun_out/pmc_r3q.log; exit 1; }
 echo pmc ok
-MZGO_LIB=$PWD/muzero-go_amd/mzgo/libmzgo_stamps.so timeout -k 10 300 python scripts/phases.py r3p > gpurun_out/phases_r3p.log 2>&1 || { tail -5 gpurun_out/phases_r3p.log; exit 1; }
+MZGO_LIB=$PWD/muzero-go_amd/mzgo/libmzgo_stamps.so timeout -k 10 300 python scripts/phases.py r3q > gpurun_out/phases_r3q.log 2>&1 || { tail -5 gpurun_out/phases_r3q.log; exit 1; }
 echo phases ok
 timeout -k 10 300 python bench.py > gpurun_out/b_default.json 2>&1 || { tail -5 gpurun_out/b_default.json; exit 1; }
 echo "default $(tail -1 gpurun_out/b_default.json | cut -c1-200)"
@@ -17,3 +17,5 @@ timeout -k 10 200 python bench.py --board-size 19 --games 64 --sims 800 --steps 
 echo "19x19 $(tail -1 gpurun_out/g19.json | cut -c1-200)"
 timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline > gpurun_out/c5.json 2>&1 || { tail -5 gpurun_out/c5.json; exit 1; }
 echo "c5 $(tail -1 gpurun_out/c5.json | cut -c1-200)"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -5 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
