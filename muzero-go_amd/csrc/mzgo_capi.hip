@@ -594,7 +594,7 @@ int mzgo_search(mzgo_engine* e, const float* root_obs, const double* noise, int 
     HIPCHK(t.ts->obs_search(t.TA, sp, root_obs, e->cfg.game_base, move_index, G, s));
     HIPCHK(t.root_phase(sp, e->E, noise, e->A, 0, s));
     HIPCHK(t.simulations(sp, e->E, s));
-    HIPCHK(t.ts->search_out(e->E, G, visits, value, s));
+    HIPCHK(t.ts->search_out(t.TA, sp, e->E, G, visits, value, s));
     return MZGO_OK;
   }
   HIPCHK(e->ks->search(e->np, e->search_params(), e->E, root_obs, noise, G, e->cfg.game_base, move_index,

@@ -1073,9 +1073,19 @@ __global__ void __launch_bounds__(64) k_texpand(TowerArrays T, SearchParams sp, 
   heads_value<G, 1>(hp, true, t.hsc, r, v);
   float x[G::AP];
   logits_regs<G, 1>(hp, true, t.hsc, x);
-  int* crow = TV.child + (size_t)nid * G::A;
-  for (int i = threadIdx.x; i < G::A; i += 64) crow[i] = -1;
-  child_priors<G>(t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant);
+  // lazy child priors (as the main engine's HBM trees): the new node's prior
+  // row keeps its policy logits and its child row the sentinel kRawRow in
+  // entry 0; select_leaf forms the priors (softmax x root mask, numpy-order
+  // sum) and the -1 child row when a select first reaches the node -- most
+  // leaves never are, so most softmaxes disappear from the simulation
+  {
+    float* prow = TV.prior + (size_t)nid * G::A;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
+    if (lane == 0) TV.child[(size_t)nid * G::A] = kRawRow;
+  }
   if (threadIdx.x == 0) acc.init(nid);
   if (threadIdx.x == (a & 63)) acc.set_child(leaf, a, nid);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1144,9 +1154,32 @@ __global__ void __launch_bounds__(64) k_tchoose(TowerArrays T, SearchParams sp, 
   }
 }
 
+// search API end: every prior row a select never reached (lazy, k_texpand)
+// turned into priors, so exported trees are complete (as k_search's
+// settle_all_priors); then the root visits / value
 template <int N>
-__global__ void __launch_bounds__(64) k_tsearch_out(EngineArrays E, int* out_visits, double* out_value) {
-  search_outputs<TGeo<N>>(E, blockIdx.x, out_visits, out_value);
+__global__ void __launch_bounds__(64) k_tsearch_out(TowerArrays T, SearchParams sp, EngineArrays E, int* out_visits,
+                                                    double* out_value) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  __shared__ TreeLds<G> t;
+  tload_mask<G>(t, T, g);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  const int lane = threadIdx.x & 63, nodes = E.nodes[g];
+  for (int n = 1; n < nodes; ++n) {
+    int* crow = TV.child + (size_t)n * G::A;
+    if (__builtin_amdgcn_readfirstlane(crow[0]) != kRawRow) continue;
+    float* prow = TV.prior + (size_t)n * G::A;
+    float x[G::AP], q[G::AP];
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j) x[j] = lane + 64 * j < G::A ? prow[lane + 64 * j] : 0.f;
+    child_prior_regs<G>(t, x, q, sp.variant, t.fbuf, t.dbuf);
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (lane + 64 * j < G::A) { prow[lane + 64 * j] = q[j]; crow[lane + 64 * j] = -1; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  search_outputs<G>(E, g, out_visits, out_value);
 }
 
 // ---------------------------------------------------------------------------

@@ -23,7 +23,8 @@ struct TowerSet {
   hipError_t (*expand)(const TowerArrays&, const SearchParams&, const EngineArrays&, int G, hipStream_t);
   hipError_t (*choose)(const TowerArrays&, const SearchParams&, const PlayParams&, const EngineArrays&, int G,
                        hipStream_t);
-  hipError_t (*search_out)(const EngineArrays&, int G, int* visits, double* value, hipStream_t);
+  hipError_t (*search_out)(const TowerArrays&, const SearchParams&, const EngineArrays&, int G, int* visits,
+                           double* value, hipStream_t);
   hipError_t (*tin)(const float* src, bf16* dst, int B, int C, int obs6, long long dst_stride, hipStream_t);
   hipError_t (*tout)(const bf16* src, float* dst, int B, int C, hipStream_t);
   hipError_t (*theads)(const TowerArrays&, int B, int has_reward, float* reward, float* value, float* logits,
@@ -80,8 +81,9 @@ struct TLaunch {
     hipLaunchKernelGGL((k_tchoose<N>), dim3(G), dim3(64), 0, s, T, sp, pp, E);
     return hipGetLastError();
   }
-  static hipError_t search_out(const EngineArrays& E, int G, int* visits, double* value, hipStream_t s) {
-    hipLaunchKernelGGL((k_tsearch_out<N>), dim3(G), dim3(64), 0, s, E, visits, value);
+  static hipError_t search_out(const TowerArrays& T, const SearchParams& sp, const EngineArrays& E, int G,
+                               int* visits, double* value, hipStream_t s) {
+    hipLaunchKernelGGL((k_tsearch_out<N>), dim3(G), dim3(64), 0, s, T, sp, E, visits, value);
     return hipGetLastError();
   }
   static hipError_t tin(const float* src, bf16* dst, int B, int C, int obs6, long long dst_stride, hipStream_t s) {
