@@ -224,7 +224,7 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
 PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
-def tower_roofline(N, C, blocks, G, sims, tower_ms, towers):
+def tower_roofline(N, C, blocks, G, sims, tower_ms, towers, towers_run):
     """Config 5's dominant kernel: k_tconv (one 3x3 conv of every active
     leaf, bf16 MFMA).  Algorithmic FLOPs per launch = boards x 2 x N^2 x 9 x C^2
     (the conv as the network defines it; the kernel also multiplies the
@@ -232,8 +232,8 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, towers):
     over the average launch duration = the timed towers' event spans / the
     2*blocks+1 launches of a tower (so the inter-launch gaps are included)."""
     L = 2 * blocks + 1
-    avg_launch_s = tower_ms / 1e3 / max(towers, 1) / L
-    boards = sims / max(towers, 1)                       # leaves evaluated per tower (terminal leaves skip)
+    avg_launch_s = tower_ms / 1e3 / max(towers, 1) / L   # (towers: the timed ones, every 16th)
+    boards = sims / max(towers_run, 1)                   # leaves evaluated per tower (terminal leaves skip)
     alg = boards * 2 * N * N * 9 * C * C
     exe = boards * 2 * 16 * ((N * N + 15) // 16) * 9 * C * C
     ach = alg / avg_launch_s / 1e12
@@ -244,7 +244,7 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, towers):
            "flops_per_launch": alg, "executed_flops_per_launch": exe,
            "mfma_executed_tflops": exe / avg_launch_s / 1e12,
            "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board) / average k_tconv launch time "
-                   "(HIP events around each simulation's tower / its launches, gaps included)"}
+                   "(HIP events around every 16th simulation's tower / its launches, gaps included)"}
     path = os.path.join(ROOT, "profiles", "latest_tower_pmc.json")
     if os.path.exists(path):
         p = json.load(open(path))
@@ -314,7 +314,7 @@ def tower_main(args, world, rank, local, cpu_ref):
         dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
     if rank == 0:
         workload = f"{N}x{N} Go self-play, {B}-block residual nets (C={C}), {G} parallel games/GPU, {S} sims/move"
-        roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers)
+        roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers, S * args.steps)
         out = {
             "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {B}-block residual "
                       f"nets, {S} sims/move (BASELINE config 5)",

@@ -65,7 +65,10 @@ struct TowerHost {
   HeadScalars hs{};
 
   // optional timing of the dynamics towers (bench.py --config 5): one event
-  // pair around each simulation step's tower, on the launch stream
+  // pair around every kTimeEvery-th simulation step's tower, on the launch
+  // stream (an event record between two kernels costs a ~3 us dispatch gap:
+  // around every tower that was 0.5 % of the simulation time)
+  static constexpr int kTimeEvery = 16;
   bool timing = false;
   std::vector<hipEvent_t> evs;
   size_t ev_used = 0;
@@ -263,12 +266,13 @@ struct TowerHost {
   hipError_t simulations(const SearchParams& sp, const EngineArrays& E, hipStream_t s) {
     hipError_t e;
     for (int i = 0; i < S; ++i) {
+      const bool tm = i % kTimeEvery == 0;
       if ((e = ts->select(TA, sp, E, G, s)) != hipSuccess) return e;
-      if ((e = mark(s)) != hipSuccess) return e;
+      if (tm && (e = mark(s)) != hipSuccess) return e;
       if ((e = tower(dyn, TA.pool, TA.in_idx, slot(), TA.pool, TA.out_idx, slot(), TA.act, TA.evalact, G, t0, t1,
                      TA.hpart, s)) != hipSuccess)
         return e;
-      if ((e = mark(s)) != hipSuccess) return e;
+      if (tm && (e = mark(s)) != hipSuccess) return e;
       if ((e = ts->expand(TA, sp, E, G, s)) != hipSuccess) return e;
     }
     if (timing) return harvest();
