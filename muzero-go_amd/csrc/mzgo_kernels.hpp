@@ -1014,7 +1014,7 @@ constexpr int verify_depth() { return G::AP > 2 ? 2 : 8; }
 // leaves deeper than this replay their batch one select at a time instead
 // (MZGO_VERIFY_MAX_DEPTH to compare the two; the trees are the same)
 #ifndef MZGO_PICK_ALL
-#define MZGO_PICK_ALL 0   // unshared batches: picks one by one, streamed (0) or all at once (1)
+#define MZGO_PICK_ALL 1   // unshared batches: picks one by one, streamed (0) or all at once (1; round 3: +0.6 %)
 #endif
 #ifdef MZGO_VERIFY_MAX_DEPTH
 constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
