@@ -1021,6 +1021,23 @@ constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
 #else
 constexpr int kVerifyMaxDepth = 1 << 20;
 #endif
+// batches of fewer children replay one select at a time (unshared batches;
+// the trees are the same either way).  Sweep of the minimum (9x9 / 256 / 200
+// epoch, same call): 2 (every batch in parallel) 75.6 M sims/s, 3 75.1,
+// 4 76.1, 6 77.1, 8 77.0, 12 74.1, 16 70.2, never 38.3
+#ifndef MZGO_VERIFY_MIN_B
+#define MZGO_VERIFY_MIN_B 6
+#endif
+constexpr int kVerifyMinB = MZGO_VERIFY_MIN_B;
+#ifndef MZGO_VERIFY_SEQ_K
+#define MZGO_VERIFY_SEQ_K 0
+#endif
+// (B - 1) * (depth + 1) < K: the batch's B - 1 replayed selects (a walk of
+// depth + 1 levels each) against the parallel replay's fixed cost
+__device__ __forceinline__ bool replay_sequential(int B, int depth) {
+  if constexpr (MZGO_VERIFY_SEQ_K > 0) return (B - 1) * (depth + 1) < MZGO_VERIFY_SEQ_K;
+  else return B < kVerifyMinB;
+}
 
 // Phase 1a of verify_batch for one path level l (row k of vl): its
 // children's c_puct * P, q, 1 / (1 + n), n and eligibility, the min / max of
@@ -1668,7 +1685,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         }
         __syncthreads();
         st.lap(5);
-        if (depth <= kVerifyMaxDepth) {
+        if (depth <= kVerifyMaxDepth && (shared_jobs<G>(sp) || !replay_sequential(B, depth))) {
           const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st, shared_jobs<G>(sp));
           nodes += m;
           sim += m;
