@@ -5,9 +5,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash scripts/pmc_selfplay.sh r3q > gpurun_out/pmc_r3q.log 2>&1 || { tail -20 gpurun_out/pmc_r3q.log; exit 1; }
+bash scripts/pmc_selfplay.sh r3r > gpurun_out/pmc_r3r.log 2>&1 || { tail -20 gpurun_out/pmc_r3r.log; exit 1; }
 echo pmc ok
-MZGO_LIB=$PWD/muzero-go_amd/mzgo/libmzgo_stamps.so timeout -k 10 300 python scripts/phases.py r3q > gpurun_out/phases_r3q.log 2>&1 || { tail -5 gpurun_out/phases_r3q.log; exit 1; }
+MZGO_LIB=$PWD/muzero-go_amd/mzgo/libmzgo_stamps.so timeout -k 10 300 python scripts/phases.py r3r > gpurun_out/phases_r3r.log 2>&1 || { tail -5 gpurun_out/phases_r3r.log; exit 1; }
 echo phases ok
 timeout -k 10 300 python bench.py > gpurun_out/b_default.json 2>&1 || { tail -5 gpurun_out/b_default.json; exit 1; }
 echo "default $(tail -1 gpurun_out/b_default.json | cut -c1-200)"
