@@ -1031,7 +1031,7 @@ constexpr int kVerifyMaxDepth = 1 << 20;
 constexpr int kVerifyMinB = MZGO_VERIFY_MIN_B;
 // default rule: sequential while (B - 1) * (depth + 1) < 16 (same call: the
 // minimum-B rule at 6 77.0-77.2 M sims/s; K = 8 / 12 / 16 / 24: 77.1 / 78.1 /
-// 79.0 / 77.8)
+// 79.0 / 77.8; a second call, K = 14 / 16 / 18 / 20: 78.5 / 78.8 / 78.6 / 78.5)
 #ifndef MZGO_VERIFY_SEQ_K
 #define MZGO_VERIFY_SEQ_K 16
 #endif
