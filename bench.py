@@ -4,14 +4,18 @@ BASELINE.json's metric on configs[1]: 256 parallel self-play games per GPU,
 200 simulations per move, the reference network (latent_dim 96) with
 deterministic random-init weights, fp32.  One *step* = one whole self-play
 epoch: all 256 games from the empty board until
-every one has ended, i.e. N*N = 81 launches of the fused k_selfplay_move
-kernel (each = one move of every unfinished game: observation record,
+every one has ended -- one launch of the fused k_selfplay_move kernel that
+plays every game's moves back to back (each move: observation record,
 representation + root priors, 200 simulations of select / dynamics +
 prediction / expand / backup, action choice, board step).
 
-Multi-GPU (torchrun, one process per GPU): games are sharded by global id
-(rank * G + slot); the only collective is the end-of-run RCCL gather of every
-rank's game records to rank 0 (inside the timed region); scaling "weak".
+Multi-GPU, one process per GPU: ``bench.py --gpus N`` starts the N rank
+processes itself (or runs under torch.distributed.run with --nproc-per-node
+N).  Games are sharded by global id (rank * G + slot); the only collective is
+the RCCL gather of every rank's packed game records to rank 0 after every
+epoch, inside the timed region (BASELINE config 3's trajectory gather);
+value = all ranks' simulations / the max over ranks of the timed span;
+scaling "weak".
 
 Prints ONE JSON line on rank 0.
 """
@@ -122,7 +126,7 @@ CUS, PEAK_CLK_GHZ = 256, 2.4
 
 def pmc_summary(workload, dynamics, moves_per_launch):
     """Per-launch PMC means of k_selfplay_move from rocprofv3 passes of this
-    same bench command (scripts/pmc_selfplay.sh -> profiles/<tag>_pmc.json);
+    same bench command (scripts/pmc.sh -> profiles/<tag>_pmc.json);
     only a profile of the same workload and launch structure counts."""
     import glob
     for path in [os.path.join(ROOT, "profiles", "latest_pmc.json")] + \
@@ -280,9 +284,23 @@ def tower_main(args, world, rank, local, cpu_ref):
     if world > 1:
         from mzgo import distributed as mdist
         mdist.broadcast_weights(net)
+    planes = None
+    if args.start_move > 0:
+        # mid-game (untimed): every game fast-forwarded to move ``start_move`` by
+        # self-play at 8 simulations per move on a second engine of the same
+        # network, its boards then loaded into the timed engine's slots
+        ff = mzgo.SelfPlay(net, G, 8, seed=4321, game_base=rank * G)
+        ff.reset(epoch=0)
+        ff.move(args.start_move)
+        planes = ff.engine.board_planes().cpu().numpy()
+        del ff
+        torch.cuda.empty_cache()
     sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G)
     eng = sp.engine
     sp.reset(epoch=0)
+    if planes is not None:
+        for g in range(G):
+            eng.board_set(g, planes[g])
     for _ in range(args.warmup):
         sp.move()
     torch.cuda.synchronize()
@@ -315,6 +333,8 @@ def tower_main(args, world, rank, local, cpu_ref):
     if rank == 0:
         workload = f"{N}x{N} Go self-play, {B}-block residual nets (C={C}), {G} parallel games/GPU, {S} sims/move"
         roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers, S * args.steps)
+        # the conv kernel's share of the step: launches x average launch / wall time
+        roof["share_of_step"] = roof["avg_launch_ms"] / 1e3 * (2 * B + 1) * S * args.steps / dt
         out = {
             "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {B}-block residual "
                       f"nets, {S} sims/move (BASELINE config 5)",
@@ -324,10 +344,14 @@ def tower_main(args, world, rank, local, cpu_ref):
             "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
             "moves_per_s": moves / dt,
             "config": {"workload": workload, "step": f"one move of {G} games/GPU ({S} simulations each; "
-                                                     f"{2 * B + 1} k_tconv launches per simulation)",
+                                                     f"{2 * B + 1} k_tconv launches per simulation)"
+                                                     + (f", from move {args.start_move}" if args.start_move else ""),
                        "board_size": N, "latent_dim": C, "res_blocks": B, "games_per_gpu": G,
                        "sims_per_move": S, "parallelism": f"game-sharded x{world}", "compat": "reference",
-                       "precision": "bf16 MFMA operands, fp32 accumulation, bf16 activations"},
+                       "precision": "bf16 MFMA operands, fp32 accumulation, bf16 activations",
+                       "start_move": args.start_move,
+                       "stones_at_start": None if planes is None else
+                       float((planes[:, 0] + planes[:, 1]).sum() / G)},
             "roofline": roof,
         }
         if cpu_ref is not None:
@@ -354,6 +378,7 @@ def refill_main(args, net, world, rank, local, cpu_ref):
     M = sps[0].max_moves
     streams = [torch.cuda.Stream() for _ in range(R)]
     ev = []
+    gathers = []
     step_no = [0]
 
     def one_epoch(record):
@@ -368,6 +393,10 @@ def refill_main(args, net, world, rank, local, cpu_ref):
             if record:
                 b.record(streams[r])
                 ev.append((a, b))
+                if world > 1:
+                    # every timed epoch's records to rank 0 (RCCL, ordered after this stream's epoch)
+                    from mzgo import distributed as mdist
+                    gathers.append(mdist.gather_packed(mdist.pack_engine(sps[r].engine), async_op=True))
         step_no[0] += 1
 
     for _ in range(max(args.warmup, R)):
@@ -380,6 +409,8 @@ def refill_main(args, net, world, rank, local, cpu_ref):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_epoch(True)
+    for work, _ in gathers:
+        work.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -423,12 +454,27 @@ def refill_main(args, net, world, rank, local, cpu_ref):
         dist.destroy_process_group()
 
 
+def _launch_module():
+    """mzgo/launch.py loaded by file path (standard library only): the parent
+    of ``--gpus N`` never imports the mzgo package, so it never loads
+    libmzgo.so."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_mzgo_launch", os.path.join(ROOT, "muzero-go_amd", "mzgo",
+                                                                             "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="2: 9x9 / 256 games / 200 sims (the headline, BASELINE configs[1]); "
                          "5: 19x19 / 20-block residual nets / 1600 sims / 64 games (BASELINE configs[4])")
     ap.add_argument("--blocks", type=int, default=20, help="residual blocks (config 5)")
+    ap.add_argument("--start-move", type=int, default=0,
+                    help="config 5: time moves from this move on (every game fast-forwarded there first by "
+                         "untimed self-play at 8 simulations per move)")
     ap.add_argument("--gpus", type=int, default=1)
     # defaults per config (2: 10 / 1 / 9 / 256 / 200 / 96; 5: 2 / 1 / 19 / 64 / 1600 / 256), filled below
     # only where the option is not given
@@ -458,7 +504,17 @@ def main():
         if getattr(args, k) is None:
             setattr(args, k, v)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # --gpus N without a launcher: N fresh rank processes (RANK / LOCAL_RANK /
+        # WORLD_SIZE / MASTER_* as torch.distributed.run sets them), started
+        # before anything here loads libmzgo.so or touches a GPU; rank 0 prints
+        # the line, this process exits with the ranks' status
+        sys.exit(_launch_module().spawn_ranks(
+            args.gpus, [sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: run `bench.py --gpus N` alone (it starts N ranks) "
+                 f"or under torch.distributed.run with --nproc-per-node N")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal of the N>1 path on a one-GPU box (never the driver's runs):
@@ -484,6 +540,7 @@ def main():
         return
 
     import mzgo
+    from mzgo import distributed as mdist
 
     N, C, S, G = args.board_size, args.latent_dim, args.sims, args.games
     A = N * N + 1
@@ -491,7 +548,6 @@ def main():
     if rank == 0:
         net.load_state_dict(mzgo.deterministic_state_dict(C, A, 0))
     if world > 1:
-        from mzgo import distributed as mdist
         mdist.broadcast_weights(net)                      # one RCCL broadcast, untimed
     if args.refill >= 2:
         refill_main(args, net, world, rank, local, cpu_ref)
@@ -532,14 +588,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    gathers = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         one_epoch(ev[i])
-    if world > 1:
-        # the trajectory gather of config 3: every rank's packed game records
-        # to rank 0's HBM over RCCL (the only collective on the data path)
-        from mzgo import distributed as mdist
-        mdist.gather_packed(mdist.pack_engine(eng), to_host=False)
+        if world > 1:
+            # the trajectory gather of config 3: after every epoch, every rank's
+            # packed game records to rank 0's HBM over RCCL (the only collective
+            # on the data path); asynchronous, so the next epoch's launch is
+            # queued at once and the gather runs on RCCL's stream beside it
+            gathers.append(mdist.gather_packed(mdist.pack_engine(eng), async_op=True))
+    for work, _ in gathers:
+        work.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -588,6 +648,9 @@ def main():
                        "dynamics": args.dynamics},
             "roofline": roof,
         }
+        if world > 1:
+            out["gather"] = {"collective": f"{dist.get_backend()} gather to rank 0", "per_step": 1,
+                             "count": len(gathers), "bytes_per_rank": int(gathers[0][1][0].numel()) if gathers else 0}
         ph = phases_summary(workload, args.moves_per_launch) if args.dynamics == "factored" else None
         if ph is not None:
             out["phases"] = ph

@@ -185,6 +185,25 @@ int mzgo_dyn_conv_backward(const float* grad_out, const float* out, const float*
                            const float* emb, const float* weight, int B, int C, int N, float* grad_latent,
                            float* grad_weight, float* grad_bias, void* workspace, int64_t workspace_bytes,
                            void* stream);
+/* Trainer: one 3x3 conv layer y = relu(conv3x3(x') + bias), padding 1, on
+ * fp32 MFMA (main.py:72-84 RepresentationNetwork's conv1-3, main.py:97-103
+ * DynamicsNetwork's conv), x' = x [B][Cin][N][N], or x + emb[action[b]]
+ * broadcast over the board when emb ([A][Cin]) is given (the dynamics input).
+ * Forward: the activation recomputation of the representation's hidden
+ * layers (the engine's k_initial_inference keeps them on chip).  Backward:
+ * from the saved output (ReLU mask y > 0) and input, grad_x [B][Cin][N][N]
+ * (may be NULL: the first layer), grad_weight [Cout][Cin][3][3], grad_bias
+ * [Cout]; deterministic (fixed summation order).  Replaces
+ * torch.nn.grad.conv2d_input / conv2d_weight in the trainer's autograd
+ * Functions.  Any Cin, Cout >= 1; 2 <= N <= 19; device workspace of at least
+ * mzgo_conv3x3_backward_workspace(B, Cin, Cout) bytes. */
+int mzgo_conv3x3_relu_forward(const float* x, const int64_t* action, const float* emb, const float* weight,
+                              const float* bias, int B, int Cin, int Cout, int N, float* out, void* stream);
+int mzgo_conv3x3_backward_workspace(int B, int Cin, int Cout, int64_t* bytes_host);
+int mzgo_conv3x3_backward(const float* grad_out, const float* out, const float* x, const int64_t* action,
+                          const float* emb, const float* weight, int B, int Cin, int Cout, int N, float* grad_x,
+                          float* grad_weight, float* grad_bias, void* workspace, int64_t workspace_bytes,
+                          void* stream);
 /* Test hook: use injected Dirichlet samples f64 [G][max_moves][A] (device,
  * caller-owned, must outlive the moves) instead of the counter-RNG sampler;
  * NULL restores sampling. */

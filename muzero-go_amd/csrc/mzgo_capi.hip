@@ -18,11 +18,13 @@ namespace mzgo {
 extern const KernelSet kernels_n5_c96, kernels_n6_c96, kernels_n9_c96, kernels_n19_c96, kernels_n6_c128,
     kernels_n6_c64;
 
-// the trainer's backward kernels (mzgo_train.hip)
-size_t dyn_bwd_workspace_bytes(int B, int C);
-hipError_t dyn_conv_backward(const float* g, const float* out, const float* latent, const int64_t* action,
-                             const float* emb, const float* w, int B, int C, int N, float* gx, float* gw,
-                             float* gb, void* workspace, hipStream_t s);
+// the trainer's conv layers (mzgo_train.hip)
+size_t conv_bwd_workspace_bytes(int B, int Cin, int Cout);
+hipError_t conv_forward(const float* x, const int64_t* action, const float* emb, const float* w, const float* bias,
+                        int B, int Cin, int Cout, int N, float* y, hipStream_t s);
+hipError_t conv_backward(const float* g, const float* out, const float* x, const int64_t* action, const float* emb,
+                         const float* w, int B, int Cin, int Cout, int N, float* gx, float* gw, float* gb,
+                         void* workspace, hipStream_t s);
 
 const KernelSet* find_kernels(int N, int C) {
   static const KernelSet* all[] = {&kernels_n5_c96, &kernels_n6_c96, &kernels_n9_c96, &kernels_n19_c96,
@@ -743,7 +745,7 @@ int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* str
 
 int mzgo_dyn_conv_backward_workspace(int B, int C, int64_t* bytes_host) {
   if (B < 1 || C < 16 || C % 16 || !bytes_host) return fail(MZGO_EINVAL, "bad argument (B=%d, C=%d)", B, C);
-  *bytes_host = (int64_t)dyn_bwd_workspace_bytes(B, C);
+  *bytes_host = (int64_t)conv_bwd_workspace_bytes(B, C, C);
   return MZGO_OK;
 }
 
@@ -754,11 +756,41 @@ int mzgo_dyn_conv_backward(const float* grad_out, const float* out, const float*
   if (!grad_out || !out || !latent || !action || !emb || !weight || !grad_latent || !grad_weight || !grad_bias ||
       !workspace || B < 1 || C < 16 || C % 16 || N < 2 || N > 19)
     return fail(MZGO_EINVAL, "bad argument (B=%d, C=%d, N=%d)", B, C, N);
-  if (workspace_bytes < (int64_t)dyn_bwd_workspace_bytes(B, C))
+  if (workspace_bytes < (int64_t)conv_bwd_workspace_bytes(B, C, C))
     return fail(MZGO_EINVAL, "workspace too small: %lld < %lld bytes", (long long)workspace_bytes,
-                (long long)dyn_bwd_workspace_bytes(B, C));
-  HIPCHK(dyn_conv_backward(grad_out, out, latent, action, emb, weight, B, C, N, grad_latent, grad_weight, grad_bias,
-                           workspace, (hipStream_t)stream));
+                (long long)conv_bwd_workspace_bytes(B, C, C));
+  HIPCHK(conv_backward(grad_out, out, latent, action, emb, weight, B, C, C, N, grad_latent, grad_weight, grad_bias,
+                       workspace, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_conv3x3_relu_forward(const float* x, const int64_t* action, const float* emb, const float* weight,
+                              const float* bias, int B, int Cin, int Cout, int N, float* out, void* stream) {
+  if (!x || !weight || !bias || !out || (emb && !action) || B < 1 || Cin < 1 || Cout < 1 || N < 2 || N > 19)
+    return fail(MZGO_EINVAL, "bad argument (B=%d, Cin=%d, Cout=%d, N=%d)", B, Cin, Cout, N);
+  HIPCHK(conv_forward(x, action, emb, weight, bias, B, Cin, Cout, N, out, (hipStream_t)stream));
+  return MZGO_OK;
+}
+
+int mzgo_conv3x3_backward_workspace(int B, int Cin, int Cout, int64_t* bytes_host) {
+  if (B < 1 || Cin < 1 || Cout < 1 || !bytes_host)
+    return fail(MZGO_EINVAL, "bad argument (B=%d, Cin=%d, Cout=%d)", B, Cin, Cout);
+  *bytes_host = (int64_t)conv_bwd_workspace_bytes(B, Cin, Cout);
+  return MZGO_OK;
+}
+
+int mzgo_conv3x3_backward(const float* grad_out, const float* out, const float* x, const int64_t* action,
+                          const float* emb, const float* weight, int B, int Cin, int Cout, int N, float* grad_x,
+                          float* grad_weight, float* grad_bias, void* workspace, int64_t workspace_bytes,
+                          void* stream) {
+  if (!grad_out || !out || !x || (emb && !action) || !weight || !grad_weight || !grad_bias || !workspace || B < 1 ||
+      Cin < 1 || Cout < 1 || N < 2 || N > 19)
+    return fail(MZGO_EINVAL, "bad argument (B=%d, Cin=%d, Cout=%d, N=%d)", B, Cin, Cout, N);
+  if (workspace_bytes < (int64_t)conv_bwd_workspace_bytes(B, Cin, Cout))
+    return fail(MZGO_EINVAL, "workspace too small: %lld < %lld bytes", (long long)workspace_bytes,
+                (long long)conv_bwd_workspace_bytes(B, Cin, Cout));
+  HIPCHK(conv_backward(grad_out, out, x, action, emb, weight, B, Cin, Cout, N, grad_x, grad_weight, grad_bias,
+                       workspace, (hipStream_t)stream));
   return MZGO_OK;
 }
 

@@ -8,6 +8,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic switches that change results (stage knock-outs, timing
+// ablations) exist only in diagnostic builds (mzgo_diag.hpp): the product
+// library refuses to compile with any of them.
+#if !defined(MZGO_DIAG_BUILD) &&                                                          \
+    (defined(MZGO_TCONV_ABL_NODMA) || defined(MZGO_TCONV_ABL_NOBAR) || defined(MZGO_DIAG_NOA) || \
+     defined(MZGO_DIAG_NOB) || defined(MZGO_DIAG_L1A) || defined(MZGO_DIAG_XNOE) ||               \
+     defined(MZGO_DIAG_XNOY) || defined(MZGO_DIAG_XNOW) || defined(MZGO_DIAG_YL1) ||              \
+     defined(MZGO_DIAG_NODMA) || defined(MZGO_DIAG_HELPER_SKIP))
+#error "wrong-result diagnostic switch without -DMZGO_DIAG_BUILD (diagnostic builds: scripts/build_variant.sh)"
+#endif
+
 namespace mzgo {
 
 // One workgroup per game.  9x9 runs 12 waves = 3 per SIMD (Winograd convs,

@@ -496,9 +496,8 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
 // Same LDS image, DMA pipeline and barriers as k_tconv.
 // ---------------------------------------------------------------------------
 // experiment knobs (A/B builds): MZGO_TCONV_PRIO 1 = s_setprio 1 around every
-// MFMA group, 2 = static priority for waves 4-7; MZGO_TCONV_ABL_NODMA /
-// _NOBAR = timing ablations (wrong results: no DMA after the first step / no
-// step barriers)
+// MFMA group, 2 = static priority for waves 4-7.  The timing ablations (wrong
+// results) live in mzgo_diag.hpp, compiled only into diagnostic builds.
 #ifndef MZGO_TCONV_PRIO
 #define MZGO_TCONV_PRIO 0
 #endif
@@ -507,15 +506,10 @@ constexpr int kPrio = MZGO_TCONV_PRIO;
 #define MZGO_TCONV_DMASPREAD 1
 #endif
 constexpr int kDmaSpread = MZGO_TCONV_DMASPREAD;   // > 0: one DMA piece every kDmaSpread MFMA groups
-#ifdef MZGO_TCONV_ABL_NODMA
-constexpr bool kAblNoDma = true;
+#ifdef MZGO_DIAG_BUILD
+#include "mzgo_diag.hpp"
 #else
-constexpr bool kAblNoDma = false;
-#endif
-#ifdef MZGO_TCONV_ABL_NOBAR
-constexpr bool kAblNoBar = true;
-#else
-constexpr bool kAblNoBar = false;
+constexpr bool kAblNoDma = false, kAblNoBar = false;
 #endif
 
 template <int N>
@@ -755,35 +749,49 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
   float* const set = reinterpret_cast<float*>(lds + XBYTES);          // E rows [9][64]
   float* const hxs = set + 9 * 64;                                     // head partials of kh = 1 [4][MT][16][3]
   static_assert(XBYTES + (9 * 64 + 4 * MT * 16 * 3) * 4 <= 2 * T::PB + 2 * T::WSLOT, "epilogue LDS");
-  const int row = lane >> 4, col = lane & 15;
-  auto finish = [&](auto khc) {                        // kh as a constant: no dynamic register indexing
+  // lane indices re-read here (tid_local: an empty asm), so nothing the
+  // epilogue derives from them is hoisted above the k-loop and kept live through it
+  const int elane = tid_local() & 63;
+  const int row = elane >> 4, col = elane & 15;
+  int qv[MT];
+  bool okv[MT];
+  bf16x8 r8[MT];
+  float hsum[MT][3];
+  f32x4* const xch = reinterpret_cast<f32x4*>(lds);
+  // The per-wave parts take kh as a constant (no dynamic register indexing of
+  // acc); every barrier sits between them, in code all waves run.
+  // 1. hand the partner its n-tiles; the residual pieces
+  auto give = [&](auto khc) {
     constexpr int KH = decltype(khc)::value, GIVE = KH == 0 ? 2 : 0, KEEP = 2 - GIVE;
-    f32x4* xch = reinterpret_cast<f32x4*>(lds);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int nn = 0; nn < 2; ++nn) xch[(((mg * 2 + KH) * MT + i) * 2 + nn) * 64 + lane] = acc[i][GIVE + nn];
     // this lane's piece after the swap and its 8 couts
-    const int pc = 2 * (KEEP + (row & 1)) + (row >> 1), c0 = pc * 8;
-    int qv[MT];
-    bool okv[MT];
+    const int pc = 2 * (KEEP + (row & 1)) + (row >> 1);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const int p = tcell<N>((mg * MT + i) * 16 + col);
       okv[i] = (mg * MT + i) < G::TT && p >= 0;
       qv[i] = okv[i] ? (p / N + 1) * G::W + (p % N) + 1 : 0;
     }
-    bf16x8 r8[MT];
     if (res) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
         if (okv[i]) r8[i] = *reinterpret_cast<const bf16x8*>(res + tpix(qv[i], pc));
     }
-    if (a.etab) {
-      const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
-      for (int k = tid; k < 9 * 64; k += NW * 64) set[k] = eb[(size_t)(k >> 6) * CO * 64 + (k & 63)];
-    }
-    __syncthreads();
+  };
+  if (kh == 0) give(std::integral_constant<int, 0>{});
+  else give(std::integral_constant<int, 1>{});
+  if (a.etab) {
+    const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
+    for (int k = tid; k < 9 * 64; k += NW * 64) set[k] = eb[(size_t)(k >> 6) * CO * 64 + (k & 63)];
+  }
+  __syncthreads();
+  // 2. the partner's half added, the epilogue, the head partials of kh = 1 staged
+  auto finish = [&](auto khc) {
+    constexpr int KH = decltype(khc)::value, KEEP = KH == 0 ? 0 : 2;
+    const int pc = 2 * (KEEP + (row & 1)) + (row >> 1), c0 = pc * 8;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -794,7 +802,6 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) { bias[e] = b0[e]; bias[e + 4] = b1[e]; }
     }
-    float hsum[MT][3];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       float v[8];
@@ -836,31 +843,28 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
         }
       }
     }
-    if (a.headw) {
-      // the pixel's sum over this chunk's 64 couts: (kh = 0's 32) + (kh = 1's 32)
-      if constexpr (KH == 1) {
-        if (row == 0)
+    // the pixel's head sums over this chunk's 64 couts: (kh = 0's 32) + (kh = 1's 32)
+    if (KH == 1 && a.headw && row == 0)
 #pragma unroll
-          for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int hh = 0; hh < 3; ++hh) hxs[((mg * MT + i) * 16 + col) * 3 + hh] = hsum[i][hh];
-      }
-      __syncthreads();
-      if constexpr (KH == 0) {
-        if (row == 0)
-#pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            const int p = tcell<N>((mg * MT + i) * 16 + col);
-            if (!okv[i]) continue;
-            float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
-#pragma unroll
-            for (int hh = 0; hh < 3; ++hh) hp[hh * G::CS] = hsum[i][hh] + hxs[((mg * MT + i) * 16 + col) * 3 + hh];
-          }
-      }
-    }
+        for (int hh = 0; hh < 3; ++hh) hxs[((mg * MT + i) * 16 + col) * 3 + hh] = hsum[i][hh];
   };
   if (kh == 0) finish(std::integral_constant<int, 0>{});
   else finish(std::integral_constant<int, 1>{});
+  // 3. kh = 0 stores the chunk's head partials
+  if (a.headw) {
+    __syncthreads();
+    if (kh == 0 && row == 0)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int p = tcell<N>((mg * MT + i) * 16 + col);
+        if (!okv[i]) continue;
+        float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
+#pragma unroll
+        for (int hh = 0; hh < 3; ++hh) hp[hh * G::CS] = hsum[i][hh] + hxs[((mg * MT + i) * 16 + col) * 3 + hh];
+      }
+  }
   STAMP_T(txch);
 #ifdef MZGO_TCONV_STAMPS
   if (lane == 0 && bid < 4096) {

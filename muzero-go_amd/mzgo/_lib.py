@@ -77,6 +77,9 @@ SIGNATURES = {
     "mzgo_records_pack": (_I, [_P, _P, ctypes.c_int64, _P, _P]),
     "mzgo_dyn_conv_backward_workspace": (_I, [_I, _I, ctypes.POINTER(ctypes.c_int64)]),
     "mzgo_dyn_conv_backward": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, ctypes.c_int64, _P]),
+    "mzgo_conv3x3_relu_forward": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "mzgo_conv3x3_backward_workspace": (_I, [_I, _I, _I, ctypes.POINTER(ctypes.c_int64)]),
+    "mzgo_conv3x3_backward": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_int64, _P]),
 }
 
 

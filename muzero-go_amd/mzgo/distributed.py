@@ -15,6 +15,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .launch import free_port, rank_envs, spawn_ranks  # noqa: F401  (re-exported)
+
 FIELDS = ("stones", "invd", "flags", "action", "value", "policy", "reward", "meta", "status", "final")
 
 
@@ -67,15 +69,22 @@ def pack_engine(engine):
     return buf
 
 
-def gather_packed(buf, dst=0, group=None, to_host=True):
+def gather_packed(buf, dst=0, group=None, to_host=True, async_op=False):
     """dist.gather of equal-size packed buffers to ``dst`` (device to device
-    over RCCL for CUDA tensors); host numpy arrays there if ``to_host``."""
+    over RCCL for CUDA tensors); host numpy arrays there if ``to_host``.
+
+    ``async_op``: return ``(work, parts)`` at once (parts None off ``dst``);
+    the gather is ordered after the work already on the current stream (RCCL
+    runs it on its own stream), ``work.wait()`` orders later work after it,
+    and ``to_host`` is ignored (the device tensors are returned)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if buf.is_cuda and dist.get_backend(group) == "gloo":
         buf = buf.cpu()                       # gloo gathers host tensors (CPU tests, one-GPU rehearsals)
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, parts, dst=dst, group=group)
+    work = dist.gather(buf, parts, dst=dst, group=group, async_op=async_op)
+    if async_op:
+        return work, parts
     if rank != dst:
         return None
     return [p.cpu().numpy() for p in parts] if to_host else parts

@@ -16,6 +16,7 @@ CLI (replaces ``python self_play.py``)::
 import argparse
 import os
 import pickle
+import sys
 import time
 
 import numpy as np
@@ -168,9 +169,18 @@ def main(argv=None):
     ap.add_argument("--compat", choices=["reference", "fixed"], default="reference")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--save-interval", type=int, default=10)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher N > 1 starts N child processes")
     args = ap.parse_args(argv)
     if (args.weights is None) == (args.random_init is None):
         ap.error("give exactly one of --weights or --random-init (self_play.py:531's default path is cluster-only)")
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # nothing has touched the GPU yet: one fresh process per rank
+        from .launch import spawn_ranks
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, "-m", "mzgo.selfplay",
+                                         *(sys.argv[1:] if argv is None else argv)]))
+    if args.gpus is not None and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}")
 
     # one process per GPU under torchrun: games sharded by global id, weights
     # broadcast from rank 0, finished games gathered to rank 0

@@ -24,10 +24,10 @@ on the device, every game of a batch at once) and trains on it:
   On the GPU the unroll's forward runs on the HIP kernels
   (``initial_inference_hip`` / ``recurrent_inference_hip``: the engine's
   k_initial_inference / k_recurrent_inference for the 3x3 convs, autograd
-  Functions whose backward is the HIP kernels of csrc/mzgo_train.hip for the
-  dynamics conv -- from the saved input and output -- and torch's for the
-  representation, by recomputing its hidden activations); the 1x1 heads stay
-  torch ops on the engine's latents.
+  Functions whose backward is the HIP kernels of csrc/mzgo_train.hip for every
+  3x3 conv -- the dynamics conv from its saved input and output, the
+  representation's three after recomputing its two hidden activations on the
+  same kernels); the 1x1 heads stay torch ops on the engine's latents.
 
 ``initial_inference_torch`` / ``recurrent_inference_torch`` restate
 main.py:72-144 with torch ops on the module's own parameters (reference
@@ -102,12 +102,48 @@ def recurrent_inference_torch(net, latent, action):
 # the same networks with the forward on the HIP engine (SURVEY.md §8(f) 1:
 # "forward only through HIP, backward via torch")
 # ---------------------------------------------------------------------------
+def conv3x3_forward_hip(x, weight, bias):
+    """relu(conv3x3(x) + bias), padding 1, on the HIP fp32-MFMA kernel
+    (mzgo_conv3x3_relu_forward): the representation's hidden activations
+    recomputed for its backward (main.py:72-84)."""
+    from ._lib import check, lib, ptr, stream_of
+    B, Cin, N, _ = x.shape
+    Cout = weight.shape[0]
+    dev = x.device
+    f = [t.detach().to(dev, torch.float32).contiguous() for t in (x, weight, bias)]
+    y = torch.empty(B, Cout, N, N, device=dev)
+    check(lib.mzgo_conv3x3_relu_forward(ptr(f[0]), None, None, ptr(f[1]), ptr(f[2]), B, Cin, Cout, N, ptr(y),
+                                        stream_of(dev)))
+    return y
+
+
+def conv3x3_backward_hip(g, out, x, weight, action=None, emb=None, need_input_grad=True):
+    """Backward of out = relu(conv3x3(x') + b), x' = x (+ emb[action] broadcast),
+    on the HIP kernels (mzgo_conv3x3_backward: fp32 MFMA implicit GEMMs,
+    deterministic; replaces torch.nn.grad.conv2d_input / conv2d_weight): with
+    gp = g * [out > 0], returns (d x or None, d weight, d bias)."""
+    from ._lib import check, lib, ptr, stream_of
+    B, Cin, N, _ = x.shape
+    Cout = weight.shape[0]
+    dev = x.device
+    f = [t.detach().to(dev, torch.float32).contiguous() for t in (g, out, x, weight)]
+    e = emb.detach().to(dev, torch.float32).contiguous() if emb is not None else None
+    act = action.to(dev, torch.int64).contiguous() if action is not None else None
+    ws = ctypes.c_int64()
+    check(lib.mzgo_conv3x3_backward_workspace(B, Cin, Cout, ctypes.byref(ws)))
+    work = torch.empty(ws.value, dtype=torch.uint8, device=dev)
+    gx = torch.empty_like(f[2]) if need_input_grad else None
+    gw = torch.empty_like(f[3])
+    gb = torch.empty(Cout, device=dev)
+    check(lib.mzgo_conv3x3_backward(ptr(f[0]), ptr(f[1]), ptr(f[2]), ptr(act), ptr(e), ptr(f[3]), B, Cin, Cout, N,
+                                    ptr(gx), ptr(gw), ptr(gb), ptr(work), ws.value, stream_of(dev)))
+    return gx, gw, gb
+
+
 def dyn_conv_backward_hip(g, nxt, latent, action, emb, weight):
     """The dynamics conv's backward on the HIP kernels (mzgo_dyn_conv_backward,
-    csrc/mzgo_train.hip: fp32 MFMA implicit GEMMs; replaces
-    torch.nn.grad.conv2d_input / conv2d_weight): with gp = g * [nxt > 0],
-    returns (d latent, d weight, d bias) of nxt = relu(conv3x3(latent +
-    emb[action]) + bias), main.py:97-103."""
+    csrc/mzgo_train.hip): with gp = g * [nxt > 0], returns (d latent, d weight,
+    d bias) of nxt = relu(conv3x3(latent + emb[action]) + bias), main.py:97-103."""
     from ._lib import check, lib, ptr, stream_of
     B, C, N, _ = latent.shape
     dev = latent.device
@@ -147,25 +183,26 @@ class _HipDynamicsConv(torch.autograd.Function):
 
 class _HipRepresentation(torch.autograd.Function):
     """The representation (main.py:72-84) with the forward on the engine's
-    k_initial_inference; the backward recomputes its two hidden activations
-    with torch (activation recomputation) and differentiates the torch graph."""
+    k_initial_inference and the backward on the HIP kernels: the two hidden
+    activations recomputed (mzgo_conv3x3_relu_forward; the engine keeps them
+    on chip), then each conv's input / weight / bias gradients from the saved
+    input and output (mzgo_conv3x3_backward), conv3 -> conv2 -> conv1."""
 
     @staticmethod
     def forward(ctx, obs, w1, b1, w2, b2, w3, b3, net):
         lat, _, _ = net.engine().initial_inference(obs.detach())
-        ctx.save_for_backward(obs, w1, b1, w2, b2, w3, b3)
+        ctx.save_for_backward(obs, w1, b1, w2, b2, w3, b3, lat)
         return lat
 
     @staticmethod
     def backward(ctx, g):
-        obs, *params = ctx.saved_tensors
-        with torch.enable_grad():
-            ps = [p.detach().requires_grad_(True) for p in params]
-            x = F.relu(F.conv2d(obs, ps[0], ps[1], padding=1))
-            x = F.relu(F.conv2d(x, ps[2], ps[3], padding=1))
-            lat = F.relu(F.conv2d(x, ps[4], ps[5], padding=1))
-            grads = torch.autograd.grad(lat, ps, g)
-        return (None, *grads, None)
+        obs, w1, b1, w2, b2, w3, b3, lat = ctx.saved_tensors
+        x1 = conv3x3_forward_hip(obs, w1, b1)
+        x2 = conv3x3_forward_hip(x1, w2, b2)
+        g2, gw3, gb3 = conv3x3_backward_hip(g, lat, x2, w3)
+        g1, gw2, gb2 = conv3x3_backward_hip(g2, x2, x1, w2)
+        _, gw1, gb1 = conv3x3_backward_hip(g1, x1, obs, w1, need_input_grad=False)
+        return None, gw1, gb1, gw2, gb2, gw3, gb3, None
 
 
 def initial_inference_hip(net, observation):

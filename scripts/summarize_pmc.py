@@ -1,4 +1,4 @@
-"""Summarise a scripts/pmc_selfplay.sh run into profiles/<tag>_pmc.json (and
+"""Summarise a scripts/pmc.sh run into profiles/<tag>_pmc.json (and
 profiles/latest_pmc.json, which bench.py reads) + profiles/<tag>_kernel_stats.csv.
 
 Per-launch means over every dispatch of the kernel (the trace's average

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "mzgo.h")
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(mzgo_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(mzgo_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -116,3 +116,79 @@ def test_broadcast_weights_gloo():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == {0: 0.0, 1: 0.0}
+
+
+def test_rank_envs_as_torchrun_sets_them():
+    """bench.py --gpus N / mzgo.selfplay --gpus N without a launcher: the
+    environment each rank process gets (the one torch.distributed.run gives)."""
+    from mzgo.launch import rank_envs
+    base = {"HSA_ENABLE_IPC_MODE_LEGACY": "0", "PATH": "/usr/bin", "KEEP": "x"}
+    envs = rank_envs(8, base, master_port=29999)
+    assert len(envs) == 8
+    for r, e in enumerate(envs):
+        assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"], e["LOCAL_WORLD_SIZE"]) == (str(r), str(r), "8", "8")
+        assert (e["MASTER_ADDR"], e["MASTER_PORT"]) == ("127.0.0.1", "29999")
+        assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["KEEP"] == "x"
+    assert "RANK" not in base                       # the parent's environment is not modified
+    ports = {e["MASTER_PORT"] for e in rank_envs(2, base)}
+    assert len(ports) == 1 and int(ports.pop()) > 0
+
+
+def test_spawn_ranks_runs_every_rank(tmp_path):
+    import sys
+    from mzgo.launch import spawn_ranks
+    code = ("import os, pathlib; e = os.environ; "
+            "pathlib.Path(r'%s', e['RANK']).write_text(','.join(e[k] for k in "
+            "('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')))" % tmp_path)
+    assert spawn_ranks(3, [sys.executable, "-c", code]) == 0
+    got = sorted(p.read_text() for p in tmp_path.iterdir())
+    assert got == [f"{r},{r},3,127.0.0.1" for r in range(3)]
+
+
+def test_spawn_ranks_stops_the_others_when_a_rank_fails():
+    """A failed rank ends the run with its status; a peer stuck (e.g. in a
+    collective) is terminated instead of outliving it."""
+    import sys
+    import time
+    from mzgo.launch import spawn_ranks
+    code = "import os, sys, time; r = int(os.environ['RANK']); time.sleep(0.5) if r == 1 else time.sleep(600); " \
+           "sys.exit(3)"
+    t0 = time.time()
+    assert spawn_ranks(2, [sys.executable, "-c", code]) == 3
+    assert time.time() - t0 < 60
+
+
+def _per_epoch_worker(rank, world, port, out):
+    """Every epoch's packed records gathered asynchronously (bench.py's
+    timed loop), waited on at the end: rank 0 holds each epoch's buffers
+    from every rank, in order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        works = []
+        for epoch in range(3):
+            buf = torch.full((64,), 10 * epoch + rank, dtype=torch.uint8)
+            works.append(mdist.gather_packed(buf, async_op=True))
+        for w, _ in works:
+            w.wait()
+        if rank == 0:
+            out.put([[int(p[0]) for p in parts] for _, parts in works])
+        else:
+            assert all(parts is None for _, parts in works)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_every_epoch_async_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_per_epoch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == [[0, 1], [10, 11], [20, 21]]

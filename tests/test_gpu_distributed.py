@@ -40,3 +40,42 @@ def test_sharded_selfplay_cli_equals_single_process(tmp_path):
     assert names and names == sorted(os.listdir(two))
     match, mismatch, errors = filecmp.cmpfiles(one, two, names, shallow=False)
     assert not mismatch and not errors, (mismatch, errors)
+
+
+def test_selfplay_cli_gpus_flag_starts_the_ranks(tmp_path):
+    """``python -m mzgo.selfplay --gpus 2`` without a launcher: the CLI starts
+    its two rank processes itself; same batches as one process."""
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "muzero-go_amd") + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               MZGO_SHARE_DEVICE="1", MZGO_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    args = ["--random-init", "0", "--board-size", "9", "--num_games", "6", "--simulations", "16",
+            "--save-interval", "3"]
+    one, two = tmp_path / "one", tmp_path / "two"
+    _run([sys.executable, "-m", "mzgo.selfplay", *args, "--output_dir", str(one)], env)
+    _run([sys.executable, "-m", "mzgo.selfplay", *args, "--gpus", "2", "--output_dir", str(two)], env)
+    names = sorted(os.listdir(one))
+    assert names and names == sorted(os.listdir(two))
+    match, mismatch, errors = filecmp.cmpfiles(one, two, names, shallow=False)
+    assert not mismatch and not errors, (mismatch, errors)
+
+
+def test_bench_gpus_2_starts_two_ranks_and_gathers_every_epoch():
+    """``bench.py --gpus 2`` as the driver runs it (no launcher): two rank
+    processes (here both on cuda:0 with gloo standing in for RCCL), one
+    record gather per timed epoch, n_gpus 2 in the rank-0 line."""
+    import json
+    env = dict(os.environ, MZGO_SHARE_DEVICE="1", MZGO_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline"], env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3
+    assert out["config"]["parallelism"] == "game-sharded x2"
+    assert out["gather"]["count"] == 3 and out["gather"]["per_step"] == 1
+    assert out["gather"]["bytes_per_rank"] > 256 * 81 * 82 * 8
+    assert out["value"] > 0

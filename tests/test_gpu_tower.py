@@ -252,3 +252,53 @@ def test_tower_mksplit_kernel_matches_oracle():
                        timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "5 passed" in r.stdout, r.stdout[-1000:]
+
+
+# Config 5's real network (19x19, C=256, 20 blocks) in a search: the engine's
+# tree vs oracle.mcts.MCTS driven by OracleResNet(bf16=True) with the same
+# counter streams and injected noise (SURVEY.md §4, bf16 mode: "root value
+# within tolerance and bounded visit-count L1").  Positions with few legal
+# moves, so that most simulations after the root's children are expanded
+# choose by PUCT -- the phase where values decide the tree.  Bounds: root
+# value |diff| <= C5_VALUE_TOL, root-child visit L1 <= C5_VISIT_L1 (values
+# observed on the MI355X in DESIGN.md §4b).
+C5_TREE_CASES = [(300, 1, 160), (400, 2, 128), (0, 0, 64)]   # (random moves, seed, simulations)
+C5_VALUE_TOL = 2e-3
+C5_VISIT_L1 = 8
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("moves,seed,S", C5_TREE_CASES, ids=[f"m{m}_s{s}_S{S}" for m, s, S in C5_TREE_CASES])
+def test_tower_config5_tree_bounded(moves, seed, S):
+    import json
+    import mzgo
+    from oracle.mcts import MCTS as OracleMCTS, tree_summary
+    from oracle.positions import random_position
+    from oracle.rng import SearchHooks, injected_noise
+    N, C, blocks = 19, 256, 20
+    A = N * N + 1
+    net, emu, _ = _nets(N, C, blocks)
+    obs = random_position(N, moves, seed).astype(np.float64)
+    sseed, game, move = 17, 5, moves
+    noise = injected_noise(sseed, game, move, A)
+    m = mzgo.MCTS(net, A, S, seed=sseed, game=game)
+    _, _, value = m.run(obs, move_index=move, noise=torch.from_numpy(noise))
+    hooks = SearchHooks(sseed, game, move)
+    om = OracleMCTS(emu, A, S, choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+                    noise=lambda p, a, e: (1 - e) * p + e * noise)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(16)
+    try:
+        with torch.no_grad():
+            oroot, _, ovalue = om.run(obs)
+    finally:
+        torch.set_num_threads(nt)
+    visits, _ = tree_summary(oroot, A)
+    got = np.asarray(m.root_child_visits, np.int64)
+    l1 = int(np.abs(got - visits).sum())
+    legal = int((gg.invalid_moves(obs) == 0).sum())
+    print(json.dumps({"case": [moves, seed, S], "legal": legal, "root_value": value, "oracle_root_value": ovalue,
+                      "value_diff": abs(value - ovalue), "visit_l1": l1, "identical": l1 == 0}))
+    assert got.sum() == visits.sum()
+    assert l1 <= C5_VISIT_L1, (l1, got[got != visits], visits[got != visits])
+    assert abs(value - ovalue) <= C5_VALUE_TOL, (value, ovalue)

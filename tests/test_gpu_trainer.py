@@ -183,3 +183,57 @@ def test_dyn_conv_backward_hip_matches_torch(N, C, B):
     torch.testing.assert_close(gx, rx, atol=1e-5, rtol=1e-4)
     torch.testing.assert_close(gw, rw, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(gb, rb, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,B", [(5, 6, 64, 7), (9, 64, 64, 3), (6, 64, 96, 17), (19, 6, 64, 2),
+                                          (9, 64, 128, 9)])
+def test_conv3x3_layer_hip_matches_torch(N, Cin, Cout, B):
+    """The representation's conv layers on the HIP kernels
+    (mzgo_conv3x3_relu_forward: the activation recomputation;
+    mzgo_conv3x3_backward: input / weight / bias gradients) against torch at
+    the shapes of main.py:72-84 (conv1 6 -> 64, conv2 64 -> 64, conv3 64 ->
+    C).  fp32, different summation order: forward |diff| <= 1e-5 + 1e-5 |ref|;
+    gx <= 1e-5 + 1e-4 |ref|, gw / gb <= 1e-4 + 1e-4 |ref|."""
+    from mzgo.trainer import conv3x3_backward_hip, conv3x3_forward_hip
+    gen = torch.Generator().manual_seed(N * 1000 + Cin * 7 + Cout + B)
+    x = torch.randn(B, Cin, N, N, generator=gen).relu().cuda()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=gen) / (3 * Cin ** 0.5)).cuda()
+    bias = (torch.randn(Cout, generator=gen) * 0.1).cuda()
+    y = conv3x3_forward_hip(x, w, bias)
+    ref = torch.relu(torch.nn.functional.conv2d(x, w, bias, padding=1))
+    torch.testing.assert_close(y, ref, atol=1e-5, rtol=1e-5)
+    g = torch.randn(B, Cout, N, N, generator=gen).cuda()
+    gx, gw, gb = conv3x3_backward_hip(g, ref, x, w)
+    gp = g * (ref > 0).float()
+    torch.testing.assert_close(gx, torch.nn.grad.conv2d_input(x.shape, w, gp, padding=1), atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(gw, torch.nn.grad.conv2d_weight(x, w.shape, gp, padding=1), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(gb, gp.sum(dim=(0, 2, 3)), atol=1e-4, rtol=1e-4)
+    none, gw2, gb2 = conv3x3_backward_hip(g, ref, x, w, need_input_grad=False)
+    assert none is None
+    assert torch.equal(gw2, gw) and torch.equal(gb2, gb)          # deterministic
+
+
+def test_representation_backward_is_hip():
+    """initial_inference_hip's backward runs the HIP conv kernels, not torch:
+    its parameter gradients equal those assembled from conv3x3_backward_hip
+    directly, bit for bit."""
+    import mzgo
+    from mzgo.trainer import conv3x3_backward_hip, conv3x3_forward_hip, initial_inference_hip
+    N, C, B = 9, 96, 5
+    A = N * N + 1
+    net = mzgo.MuZeroNet(C, A).cuda()
+    net.load_state_dict(mzgo.deterministic_state_dict(C, A, 3))
+    gen = torch.Generator().manual_seed(5)
+    obs = (torch.rand(B, 6, N, N, generator=gen) > 0.6).float().cuda()
+    lat, _, _ = initial_inference_hip(net, obs)
+    g = torch.randn(lat.shape, generator=gen).cuda()
+    net.zero_grad()
+    lat.backward(g)
+    r = net.representation
+    x1 = conv3x3_forward_hip(obs, r.conv1.weight, r.conv1.bias)
+    x2 = conv3x3_forward_hip(x1, r.conv2.weight, r.conv2.bias)
+    g2, gw3, _ = conv3x3_backward_hip(g, lat.detach(), x2, r.conv3.weight)
+    g1, gw2, _ = conv3x3_backward_hip(g2, x2, x1, r.conv2.weight)
+    _, gw1, _ = conv3x3_backward_hip(g1, x1, obs, r.conv1.weight, need_input_grad=False)
+    for got, want in ((r.conv3.weight.grad, gw3), (r.conv2.weight.grad, gw2), (r.conv1.weight.grad, gw1)):
+        assert torch.equal(got, want)
