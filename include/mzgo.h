@@ -116,10 +116,12 @@ int mzgo_search(mzgo_engine* eng, const float* root_obs, const double* noise, in
 /* Copy slot g's last search tree to host buffers (synchronises ``stream``):
  * n_nodes; child i32 [n][A]; visits i32 [n]; value_sum f64 [n]; prior f32 [n][A]
  * (row 0 unused); root_prior f64 [A].  Buffers must hold S+1 nodes; NULL skips.
- * After mzgo_search every row is final.  After mzgo_selfplay_move, the rows
- * of nodes that no select reached may still hold the child's policy logits
- * (prior) and stale ids (child): both are formed when a select first reaches
- * a node (it has no children before), and the move never reads the others. */
+ * After mzgo_search every row is final.  After mzgo_selfplay_move on the
+ * reference network (tower = 0), the rows of nodes that no select reached may
+ * still hold the child's policy logits (prior) and stale ids (child): both
+ * are formed when a select first reaches a node (it has no children before),
+ * and the move never reads the others.  Tower engines settle such rows here
+ * first (the search API's settle kernel), so their exports are complete. */
 int mzgo_tree_export(mzgo_engine* eng, int g, int32_t* n_nodes_host, int32_t* child_host,
                      int32_t* visits_host, double* value_sum_host, float* prior_host,
                      double* root_prior_host, void* stream);
@@ -140,18 +142,22 @@ int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uin
 
 /* Self-play.  selfplay_reset starts a new game in every slot (epoch = RNG
  * generation of the games); selfplay_move plays one move in every unfinished
- * slot.  selfplay_counters (host u64 [5], synchronises; cumulative over the
+ * slot.  selfplay_counters (host u64 [6], synchronises; cumulative over the
  * engine's life): [0] simulations run, [1] moves played, [2] games finished,
  * [3] slots still playing now, [4] dynamics 3x3 convs run by searches (one per
- * expansion with direct_dynamics, one per new parent node when factored). */
+ * expansion with direct_dynamics, one per new parent node when factored),
+ * [5] of those, parent convs shared with the workgroups of games that had
+ * already ended (9x9 whole-game launches: the epoch tail). */
 int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
 /* Up to ``moves`` consecutive moves of every unfinished slot in ONE launch
  * (each slot stops at its game's end); the records and RNG streams are those
  * of ``moves`` mzgo_selfplay_move calls.  moves = max_moves plays whole games.
- * Tower engines (tower = 1) run a move as a sequence of launches; they check
- * the slots' status every 4 moves (synchronising the stream) and stop
- * enqueueing once every game has ended. */
+ * Tower engines (tower = 1) run a move as a sequence of launches; for
+ * moves > 4 they read the slots' status every 4 moves (BLOCKING: the stream is
+ * synchronised there, so such a call cannot be captured in a HIP graph) and
+ * stop enqueueing once every game has ended -- the same records and counters
+ * as ``moves`` single-move calls.  moves <= 4 never synchronises. */
 int mzgo_selfplay_moves(mzgo_engine* eng, int moves, void* stream);
 
 /* Arena (main.py:526-611, SelfPlayEvaluator): like mzgo_selfplay_move, but

@@ -323,6 +323,7 @@ struct mzgo_engine {
     sp.seed = cfg.seed;
     sp.helpers = 0;
     sp.net = 0;
+    sp.tail = 0;
     return sp;
   }
 };
@@ -466,14 +467,14 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   chk(e->alloc(&E.game_len, G));
   chk(e->alloc(&E.final_reward, G));
   chk(e->alloc(&E.status, G));
-  chk(e->alloc(&E.counters, 4));
+  chk(e->alloc(&E.counters, 5));
   chk(e->alloc(&e->d_err, 1));
 #ifdef MZGO_STAMPS
   chk(e->alloc(&E.stamps, G * kStampPhases));
   if (E.stamps) (void)hipMemset(E.stamps, 0, G * kStampPhases * 8);
 #endif
   if (rc != MZGO_OK) { delete e; return rc; }
-  if (hipMemset(E.counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+  if (hipMemset(E.counters, 0, 5 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess) {
     delete e;
     return fail(MZGO_EHIP, "hipMemset failed");
@@ -609,6 +610,13 @@ int mzgo_tree_export(mzgo_engine* e, int g, int32_t* n_nodes, int32_t* child, in
   if (!e || e->C == 0 || g < 0 || g >= e->G) return fail(MZGO_EINVAL, "bad argument");
   hipStream_t s = (hipStream_t)stream;
   const size_t n1 = (size_t)e->S + 1, A = e->A;
+  if (e->tower) {
+    // rows a select never reached still hold logits + the kRawRow sentinel
+    // after a self-play move (lazy child priors): settle them as the search
+    // API does (k_tsearch_out; idempotent, the values a later select would form)
+    TowerHost& t = *e->tower;
+    HIPCHK(t.ts->search_out(t.TA, e->search_params(), e->E, e->G, nullptr, nullptr, s));
+  }
   int nn = 0;
   HIPCHK(hipMemcpyAsync(&nn, e->E.nodes + g, sizeof(int), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -669,6 +677,15 @@ static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayPara
     if (const char* v = getenv("MZGO_HELPERS_PER_GAME")) per = atoi(v);
     sp.helpers = per > 0 ? per * e->G : 0;
     HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
+  } else if (e->ks->tail_convs && sp.factored && pp.moves > 1) {
+    // the epoch tail (one-strip Winograd boards, whole games per launch): a
+    // workgroup whose game has ended serves running games' parent convs
+    // (MZGO_TAIL_HELPERS=0 turns it off; the records are the same either way)
+    const char* v = getenv("MZGO_TAIL_HELPERS");
+    if (!(v && atoi(v) == 0)) {
+      sp.tail = 1;
+      HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
+    }
   }
   HIPCHK(e->ks->selfplay_move(e->np, np_b, sp, pp, e->E, e->G, s));
   return MZGO_OK;
@@ -815,14 +832,14 @@ int mzgo_selfplay_inject_noise(mzgo_engine* e, const double* noise) {
 int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   if (!e || !out) return fail(MZGO_EINVAL, "bad argument");
   hipStream_t s = (hipStream_t)stream;
-  unsigned long long c[4] = {0, 0, 0, 0};
+  unsigned long long c[5] = {0, 0, 0, 0, 0};
   std::vector<int> st(e->G);
   HIPCHK(hipMemcpyAsync(c, e->E.counters, sizeof c, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   int playing = 0;
   for (int v : st) playing += v == 0;
-  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing; out[4] = c[3];
+  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing; out[4] = c[3]; out[5] = c[4];
   return MZGO_OK;
 }
 

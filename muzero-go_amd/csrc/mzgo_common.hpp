@@ -86,7 +86,9 @@ __host__ __device__ __forceinline__ uint32_t randbelow(uint64_t h, uint32_t n) {
 // deltas per phase into mzgo_stamps[block][phase].
 // ---------------------------------------------------------------------------
 // 0-7 phases (thread 0), 8-19 per-wave conv loops, 20-31 sub-phases,
-// 40-43 shared batch jobs (publish, picks, own rounds, wait), 52-54 shared
+// 40-43 shared batch jobs (publish, picks, own rounds, wait), 44-47 the
+// 9x9 tail (a helper's unit cycles, units, jobs served; cycles in the tail
+// phase), 52-54 shared
 // conv jobs (publish + picks, own strips, wait), 56-63 factored simulation
 // detail (see sim_loop), 64-71 batch_expand / expand_child detail,
 // 72-82 verify_batch / parent conv detail, 83-87 self-play move phases,

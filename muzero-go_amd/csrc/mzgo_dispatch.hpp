@@ -10,6 +10,7 @@ struct KernelSet {
   size_t lds_bytes;
   int rep_scratch;   // floats of HBM scratch per initial_inference item (strip boards), else 0
   int shared_batches;  // 1: the batch expansions stream Y from L2 and take helper workgroups (19x19)
+  int tail_convs;      // 1: ended games' workgroups serve running games' parent convs (9x9, tail_help)
   hipError_t (*initial_inference)(const NetParams&, const float* obs, int B, float* lat, float* val,
                                   float* logits, float* scratch, hipStream_t);
   hipError_t (*recurrent_inference)(const NetParams&, const float* lat, const int64_t* act, int B,
@@ -71,7 +72,8 @@ struct Launch {
   static KernelSet table() {
     typedef Geo<N, C> G;
     return KernelSet{N, C, sizeof(Smem<G>), rep_needs_scratch<G>() ? 64 * N * N : 0,
-                     Smem<G>::GLOBAL_Y ? 1 : 0, &ii, &ri, &search, &breset, &bstep, &bplanes,
+                     Smem<G>::GLOBAL_Y ? 1 : 0, TailConvs<G>::value ? 1 : 0, &ii, &ri, &search, &breset, &bstep,
+                     &bplanes,
                      &move};
   }
 };

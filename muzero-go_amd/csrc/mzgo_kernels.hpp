@@ -91,8 +91,9 @@ struct EngineArrays {
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
   unsigned char* jobs;   // [G][job_bytes(A)] batch-expansion jobs shared with helper workgroups
-  unsigned long long* counters;  // [4] 0: simulations run, 1: moves played, 2: games finished,
-                                 //     3: dynamics convs run (factored: one per new parent)
+  unsigned long long* counters;  // [5] 0: simulations run, 1: moves played, 2: games finished,
+                                 //     3: dynamics convs run (factored: one per new parent),
+                                 //     4: of those, tail conv jobs (conv_tail)
   unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
 };
 
@@ -514,6 +515,8 @@ struct JobView {
   __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
   // replay checks: the failing simulations found by every workgroup (bit i)
   __device__ unsigned long long* failm() const { return reinterpret_cast<unsigned long long*>(base + 256); }
+  // tail helpers registered with this game (9x9 whole-game launches, tail_help)
+  __device__ unsigned* nhelp() const { return reinterpret_cast<unsigned*>(base + 448); }
   // the actions, tagged: batch number << 32 | action (an entry is valid for
   // the batch whose number it carries: no separate progress counter)
   __device__ unsigned long long* acts() const { return reinterpret_cast<unsigned long long*>(base + 512); }
@@ -659,6 +662,165 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
   if (st) st->lap(53);
   job_wait(J, mine, Wino<G>::NSTRIP);
   if (st) st->lap(54);
+}
+
+// ---------------------------------------------------------------------------
+// The epoch tail at 9x9 (one-strip Winograd boards, the tree in LDS): in a
+// whole-game launch the games end at different moves, and the last ones
+// finish alone on their CUs (~29 % of an epoch's CU-time idle).  A workgroup
+// whose game has ended registers (JobView::nhelp) with a running game that
+// has fewer than kTailHelpers helpers and serves its parent convs: a game
+// that sees a helper registered publishes its next parent conv as a job of
+// kTailUnits units -- unit u = cout tiles 2u, 2u + 1 (wino_conv's m0 / nm) --
+// claims units itself too (it never waits for a helper to start), waits for
+// all, and loads the whole Y from L2 into its LDS copy.  Every unit computes
+// the full Winograd input (wino_input_rebuilt from the parent's Y in the pool)
+// once per job and its tiles' GEMM + epilogue exactly as the whole conv does,
+// so the records do not depend on who computed what (MZGO_TAIL_HELPERS=0 A/B).
+// Hand-offs: the job machinery above (release / relaxed flag / acquire).
+// ---------------------------------------------------------------------------
+constexpr int kTailUnits = 3;
+constexpr unsigned kTailHelpers = 2;
+constexpr int kJobTailConv = 6;        // JobView info[4] of a tail conv job
+
+template <class G>
+struct TailConvs {
+  static constexpr bool value = [] {
+    if constexpr (G::WINO) return Wino<G>::NSTRIP == 1 && !Smem<G>::GLOBAL_Y && G::C == 6 * 16;
+    else return false;
+  }();
+};
+
+// Units of tail conv job bseq of game E/g claimed by this workgroup: V from
+// the parent's Y once, then each unit's two cout tiles (red in the raw planes,
+// whose zero halo is restored afterwards); Y stores drained.  All threads.
+template <class G>
+__device__ __forceinline__ int tail_conv_units(Smem<G>& sm, const NetParams& np, const JobView& J, unsigned bseq,
+                                               const float* ypar, const float* ea, float* dst,
+                                               const float* ylds_par = nullptr) {
+  int mine = 0;
+  if constexpr (TailConvs<G>::value) {
+    for (int u; (u = job_claim(sm, J, bseq, kTailUnits, 1)) >= 0; ++mine) {
+      if (mine == 0) wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, 0, ylds_par);
+      wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.raw, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn, dst,
+                                        G::CS, G::CS, nullptr, 0, nullptr, nullptr, 2 * u, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's Y stores done
+    __syncthreads();
+    if (mine > 0) wino_raw_zero<G>(sm.raw);
+  }
+  return mine;
+}
+
+// The game's workgroup: the parent conv of node `leaf` (its latent rebuilt
+// from parent par's Y and action act's E rows) as a tail job; returns with
+// Y in the pool slot and, when ylds, in the expansion's LDS copy.  All threads.
+template <class G>
+__device__ __forceinline__ void conv_tail(Smem<G>& sm, const NetParams& np, const EngineArrays& E, int g, int leaf,
+                                          int par, int act, int net, float* dst, float* ylds, bool par_in_lds,
+                                          Stamp* st = nullptr) {
+  if constexpr (TailConvs<G>::value) {
+    const JobView J = job_of<G>(E, g);
+    const unsigned bseq = job_begin(J, kTailUnits);
+    if (tid_local() == 0) {
+      int* info = J.info();
+      info[0] = kTailUnits; info[1] = par; info[2] = leaf; info[3] = net; info[4] = kJobTailConv; info[5] = act;
+    }
+    job_publish(J, bseq);                            // (the parent's Y in the pool reaches the helpers)
+    if (st) st->lap(52);
+    const float* ypar = pool_of<G>(E, g) + (size_t)par * G::C * G::CS;
+    const int mine = tail_conv_units<G>(sm, np, J, bseq, ypar, np.etab + (size_t)act * 9 * G::C, dst,
+                                        par_in_lds ? ylds : nullptr);
+    if (st) st->lap(53);
+    job_wait(J, mine, kTailUnits);
+    if (st) st->lap(54);
+    if (tid_local() == 0) atomicAdd(&E.counters[4], 1ull);
+    if (ylds) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(dst);
+      f32x4* d = reinterpret_cast<f32x4*>(ylds);
+      for (int i = tid_local(); i < G::CELLS * G::C / 4; i += G::THREADS) d[i] = src[i];
+    }
+    __syncthreads();
+  }
+}
+
+// A workgroup whose game has ended: serve running games' tail conv jobs until
+// none is left to register with.  All threads.
+template <class G>
+__device__ __forceinline__ void tail_help(Smem<G>& sm, const NetParams& np_a, const NetParams& np_b,
+                                          const EngineArrays& E, int self, int games) {
+  if constexpr (TailConvs<G>::value) {
+    wino_raw_zero<G>(sm.raw);                          // (an ended slot's workgroup never zeroed its planes)
+    for (;;) {
+      // a running game (its seq not kJobExit) with fewer than kTailHelpers
+      // helpers, the nearest after this one
+      if (tid_local() == 0) {
+        int pick = -1;
+        for (int k = 1; k < games && pick < 0; ++k) {
+          const int t = (self + k) % games;
+          const JobView Jt = job_of<G>(E, t);
+          if (__hip_atomic_load(Jt.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kJobExit) continue;
+          unsigned c = __hip_atomic_load(Jt.nhelp(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          while (c < kTailHelpers &&
+                 !__hip_atomic_compare_exchange_strong(Jt.nhelp(), &c, c + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)) {
+          }
+          if (c < kTailHelpers) pick = t;
+        }
+        sm.bc[2] = pick;
+      }
+      __syncthreads();
+      const int t = sm.bc[2];
+      __syncthreads();
+      if (t < 0) return;
+      const JobView J = job_of<G>(E, t);
+      float* pool = pool_of<G>(E, t);
+      unsigned last = 0;
+      for (;;) {
+        if (tid_local() == 0) {
+          unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 24); ++spins) {
+            __builtin_amdgcn_s_sleep(8);
+            s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (s == last || s == 0) {                   // (bounded wait: leave this game)
+            __hip_atomic_fetch_sub(J.nhelp(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s = kJobExit;
+          }
+          if (s != kJobExit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          sm.bc[2] = (int)s;
+        }
+        __syncthreads();
+        const unsigned s = (unsigned)sm.bc[2];
+        __syncthreads();
+        if (s == kJobExit) break;
+        last = s;
+        const int* info = J.info();
+        const int par = info[1], leaf = info[2], net = info[3], kind = info[4], act = info[5];
+        if (kind != kJobTailConv) continue;
+        const NetParams np = select_params(net != 0, np_b, np_a);
+#ifdef MZGO_STAMPS
+        const unsigned long long tu = __builtin_amdgcn_s_memtime();
+#endif
+        const int mine = tail_conv_units<G>(sm, np, J, s, pool + (size_t)par * G::C * G::CS,
+                                            np.etab + (size_t)act * 9 * G::C, pool + (size_t)leaf * G::C * G::CS);
+#ifdef MZGO_STAMPS
+        // slots 44-46: a helper's cycles computing tail units, units, jobs served
+        if (tid_local() == 0 && E.stamps) {
+          unsigned long long* sl = E.stamps + (size_t)blockIdx.x * kStampPhases;
+          sl[44] += __builtin_amdgcn_s_memtime() - tu;
+          sl[45] += (unsigned long long)mine;
+          sl[46] += mine > 0 ? 1ull : 0ull;
+        }
+#endif
+        if (tid_local() == 0 && mine > 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
 }
 
 // The representation's conv2 (CIN 64 -> 64) and conv3 (64 -> C, value and
@@ -1616,8 +1778,23 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
           // fetched before the conv and stored after it: the L2 round trip
           // runs under the conv instead of after it
           if constexpr (decltype(sm.u.f)::CACHE) hwpre = tid_local() < 3 * G::C ? np.head_w[tid_local()] : 0.f;
-          latent_conv_rebuilt<G>(sm, np, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
-                                 yleaf, &st, y_lds_target<G>(sm), y_lds_target<G>(sm) != nullptr && yc == par);
+          // a tail helper registered with this game: the conv as a tail job
+          bool tail = false;
+          if constexpr (TailConvs<G>::value) {
+            if (sp.tail) {
+              if (tid_local() == 0)
+                sm.bc[3] = __hip_atomic_load(job_of<G>(E, g).nhelp(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0;
+              __syncthreads();
+              tail = sm.bc[3] != 0;
+            }
+          }
+          if (tail) {
+            conv_tail<G>(sm, np, E, g, leaf, par, nact[leaf], sp.net, yleaf, y_lds_target<G>(sm),
+                         y_lds_target<G>(sm) != nullptr && yc == par, &st);
+          } else {
+            latent_conv_rebuilt<G>(sm, np, pool + (size_t)par * node_floats, np.etab + (size_t)nact[leaf] * 9 * G::C,
+                                   yleaf, &st, y_lds_target<G>(sm), y_lds_target<G>(sm) != nullptr && yc == par);
+          }
           hwready = true;
         } else {
           latent_conv<G, G::C, G::C, 0, true>(sm, np.w_dyn, np.b_dyn, scratch, G::CS, nullptr, yleaf, G::CS,
@@ -2164,10 +2341,26 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const int g = blockIdx.x;
   const EngineArrays& E = E_arg;
   auto release_helpers = [&]() {
-    if (sp.helpers > 0 && tid_local() == 0)
+    if ((sp.helpers > 0 || sp.tail) && tid_local() == 0)
       __hip_atomic_store(job_of<G>(E_arg, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  if (E.status[g] != 0) { release_helpers(); return; }
+  // an ended game's workgroup serves running games' parent convs (9x9 epoch tail)
+  auto tail_phase = [&]() {
+    if constexpr (TailConvs<G>::value)
+      if (sp.tail) {
+        __syncthreads();
+#ifdef MZGO_STAMPS
+        const unsigned long long th = __builtin_amdgcn_s_memtime();
+#endif
+        tail_help<G>(sm, np_a_arg, np_b_arg, E_arg, g, games);
+#ifdef MZGO_STAMPS
+        // slot 47: the workgroup's cycles in the tail phase (serving + waiting)
+        if (tid_local() == 0 && E_arg.stamps) E_arg.stamps[(size_t)blockIdx.x * kStampPhases + 47] +=
+            __builtin_amdgcn_s_memtime() - th;
+#endif
+      }
+  };
+  if (E.status[g] != 0) { release_helpers(); tail_phase(); return; }
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   BoardMeta m;
   load_board<G>(sm, E, g, m);
@@ -2271,6 +2464,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   __syncthreads();                               // this move's LDS reads before the next move's writes
   }
   release_helpers();
+  tail_phase();
 }
 
 }  // namespace mzgo

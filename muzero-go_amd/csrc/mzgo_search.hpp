@@ -30,6 +30,8 @@ struct SearchParams {
   uint64_t seed;
   int helpers;              // helper workgroups sharing the batch expansions (GLOBAL_Y boards; 0: none)
   int net;                  // k_selfplay_move: the network of this move (arena: 1 = np_b), for the helpers
+  int tail;                 // 9x9 whole-game launches: a workgroup whose game has ended helps running
+                            // games with their parent convs (tail_help; 0: off)
 };
 
 // One game's tree (global memory).  Node 0 is the root; node ids grow by one

@@ -424,12 +424,18 @@ __device__ __forceinline__ constexpr float wino_at3(int ox, int j) {
 // xi = h*10 + xl and k-position k (pack_wino).  out: [COUT][out_stride]
 // global; cells >= out_cells are not stored (pooled rows, stride == out_cells
 // == CS, are stored whole with their zero pad cells).
+//
+// m0 / nm (tail helpers, 9x9 parent convs only: YM, NH = 0, one strip): only
+// cout tiles m0 .. m0 + nm - 1, on waves 0 .. 2 nm - 1; red then needs room
+// for nm tiles only and V is left intact (the next unit reuses it).  Every
+// output is computed by the same operations as in the whole conv.
 template <class G, int CIN, int COUT, int NH, bool YM = false>
 __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, float* outs, float* hfin,
                                           const float* __restrict__ upk,
                                           const float* __restrict__ bias, float* __restrict__ out,
                                           int out_stride, int out_cells, const float* __restrict__ head_w,
-                                          int strip = 0, Stamp* st = nullptr, float* ylds = nullptr) {
+                                          int strip = 0, Stamp* st = nullptr, float* ylds = nullptr, int m0 = 0,
+                                          int nm = COUT / 16) {
   typedef Wino<G> W;
   constexpr int CH = CIN / 2, S4 = CH / 16, MT = COUT / 16, XI = W::XI;
   constexpr int OS = W::OUT_STRIDE;
@@ -442,8 +448,8 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   static_assert(XH % XG == 0, "xi groups");
   const int lane = lane_id_local();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());
-  const int m = wave >> 1, h = wave & 1;
-  const bool active = wave < 2 * MT;
+  const int ml = wave >> 1, m = m0 + ml, h = wave & 1;   // (ml: the tile's slot in red)
+  const bool active = wave < 2 * nm;
   const int kq = lane >> 4, t = lane & 15;
 
   f32x4 yp[6];                                // Z [il*3 + ox] in the loop, then Y partial [oy*3 + ox]
@@ -601,7 +607,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   f32x4* red4 = reinterpret_cast<f32x4*>(red);
   if (active) {
 #pragma unroll
-    for (int ox = 0; ox < 3; ++ox) red4[((m * 2 + h) * 3 + ox) * 64 + lane] = ygive[ox];
+    for (int ox = 0; ox < 3; ++ox) red4[((ml * 2 + h) * 3 + ox) * 64 + lane] = ygive[ox];
   }
   __syncthreads();
   if (st) st->lap(7);
@@ -621,7 +627,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       ok[ox] = active && t < W::T && y < G::N && x < G::N;
       cl[ox] = y * G::N + x;
       if (active) {
-        const f32x4 other = red4[((m * 2 + (1 - h)) * 3 + ox) * 64 + lane];
+        const f32x4 other = red4[((ml * 2 + (1 - h)) * 3 + ox) * 64 + lane];
         const f32x4 mine = ymine[ox];
 #pragma unroll
         for (int r = 0; r < 4; ++r) yv[ox][r] = (h == 0 ? mine[r] + other[r] : other[r] + mine[r]) + bb[r];   // (xi half 0) + (xi half 1)
@@ -652,7 +658,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       const int cell = y * G::N + x;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float other = red4[((m * 2 + (1 - h)) * 3 + ox) * 64 + lane][r];
+        const float other = red4[((ml * 2 + (1 - h)) * 3 + ox) * 64 + lane][r];
         const float mine = ymine[ox][r];
         // fixed order: (xi half 0) + (xi half 1)
         float v = (h == 0 ? mine + other : other + mine) + bb[r];

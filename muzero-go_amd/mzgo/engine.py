@@ -222,10 +222,10 @@ class Engine:
         return ms.value, n.value
 
     def counters(self):
-        out = np.zeros(5, np.uint64)
+        out = np.zeros(6, np.uint64)
         check(lib.mzgo_selfplay_counters(self._h, ptr(out), stream_of(self.device)))
         return dict(simulations=int(out[0]), moves=int(out[1]), games_finished=int(out[2]),
-                    playing=int(out[3]), dynamics_convs=int(out[4]))
+                    playing=int(out[3]), dynamics_convs=int(out[4]), tail_convs=int(out[5]))
 
     def record(self, g):
         """Host copy of slot g's game record (numpy arrays)."""

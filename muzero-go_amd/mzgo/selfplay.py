@@ -123,7 +123,11 @@ class SelfPlay:
         self.engine.selfplay_reset(self.epoch)
 
     def move(self, moves=1):
-        """Enqueue ``moves`` moves for every unfinished game, one launch (asynchronous)."""
+        """Enqueue ``moves`` moves for every unfinished game, one launch
+        (asynchronous).  Tower engines (ResMuZeroNet) enqueue a move as a
+        sequence of launches and, for moves > 4, BLOCK every 4 moves to read
+        the games' status (mzgo_selfplay_moves): they stop once every game has
+        ended, with the records of ``moves`` single-move calls."""
         self.engine.selfplay_move(moves)
 
     def play(self):

@@ -58,10 +58,12 @@ def main():
         raise RuntimeError("mzgo_debug_stamps failed: load the -DMZGO_STAMPS build (MZGO_LIB)")
     sp.reset(epoch=1)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0 = sp.engine.counters()
     a.record()
     sp.move(sp.max_moves)
     b.record()
     torch.cuda.synchronize()
+    c1 = sp.engine.counters()
     ms = a.elapsed_time(b)
     fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))
     f = buf[:G].astype(np.float64)
@@ -83,6 +85,15 @@ def main():
                  "what": "1 - mean/max of the games' busy cycles: the CU-time the epoch leaves idle while "
                          "its slowest games finish (one game per CU)"},
         "convs_per_game": float(f[:, 59].mean()),
+        "engine_counters": {k: c1[k] - c0[k] for k in ("simulations", "dynamics_convs", "tail_convs")},
+        # the 9x9 epoch tail with tail helpers (slots 44-47): the CU-time the
+        # epoch leaves idle counts a finished game's workgroup as busy while it
+        # computes units for running games
+        "tail_helpers": {
+            "unit_cycles_per_game": float(f[:, 44].mean()), "units": float(f[:, 45].sum()),
+            "jobs_served": float(f[:, 46].sum()), "tail_phase_cycles_per_game": float(f[:, 47].mean()),
+            "idle_cu_share_with_helpers": float(1 - (game.sum() + f[:, 44].sum()) / (len(game) * game.max())),
+        },
         # every slot's mean per game (lap slots: thread 0's partition; others:
         # wave sums / counters, mzgo_common.hpp's map)
         "slots_mean_per_game": {int(i): round(float(f[:, i].mean())) for i in range(f.shape[1]) if f[:, i].any()},

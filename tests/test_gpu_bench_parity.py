@@ -252,3 +252,31 @@ def test_refill_streams_equal_one_engine():
             for k in ("value", "policy", "reward"):
                 np.testing.assert_array_equal(a[k].view(np.uint64), b[k].view(np.uint64),
                                               err_msg=f"engine {r} game {g} {k}")
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("epoch", [5, 6])
+def test_tail_helpers_do_not_change_records(epoch, monkeypatch):
+    """The 9x9 epoch tail (tail_help / conv_tail): in a whole-game launch, the
+    workgroups of ended games serve running games' parent convs.  At the
+    bench's own size (9x9 / 256 / 200, whole epoch in one launch) the records
+    and counters are byte for byte those of the same launch without it
+    (MZGO_TAIL_HELPERS=0), and the tail jobs did run."""
+    N, G, S = 9, 256, 200
+    net = _net(N)
+    sp = __import__("mzgo").SelfPlay(net, G, S, seed=SEED)
+    eng = sp.engine
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("MZGO_TAIL_HELPERS", on)
+        c0 = eng.counters()
+        sp.reset(epoch=epoch)
+        sp.move(sp.max_moves)
+        c1 = eng.counters()
+        recs, arrays = _records(eng)
+        out[on] = (recs, arrays, {k: c1[k] - c0[k] for k in c1 if k != "playing"})
+    (ra, aa, ca), (rb, ab, cb) = out["1"], out["0"]
+    assert ca["tail_convs"] > 0 and cb["tail_convs"] == 0, (ca, cb)
+    assert {k: v for k, v in ca.items() if k != "tail_convs"} == {k: v for k, v in cb.items() if k != "tail_convs"}
+    for k in aa:
+        np.testing.assert_array_equal(aa[k].view(np.uint8), ab[k].view(np.uint8), err_msg=k)
