@@ -677,6 +677,10 @@ static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayPara
     if (const char* v = getenv("MZGO_HELPERS_PER_GAME")) per = atoi(v);
     sp.helpers = per > 0 ? per * e->G : 0;
     HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
+    // the epoch tail: helpers (and workgroups) of ended games join running
+    // games (whole-game launches; MZGO_TAIL_HELPERS=0 turns it off)
+    const char* v = getenv("MZGO_TAIL_HELPERS");
+    if (sp.helpers > 0 && sp.factored && pp.moves > 1 && !(v && atoi(v) == 0)) sp.tail = 1;
   } else if (e->ks->tail_convs && sp.factored && pp.moves > 1) {
     // the epoch tail (one-strip Winograd boards, whole games per launch): a
     // workgroup whose game has ended serves running games' parent convs

@@ -1675,6 +1675,47 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
   }
 }
 
+// 19x19 epoch tail (sp.tail, whole-game launches): a helper workgroup whose
+// game has ended -- and the game's own workgroup -- move on to the running
+// game with the fewest re-assigned helpers (JobView::nhelp; the nearest after
+// `hint` among ties) and serve its jobs.  Every job kind takes any number of
+// workgroups (claims are dynamic), so this changes who computes, not what.
+// Returns the game or -1 when none is running.  All threads.
+template <class G>
+__device__ __forceinline__ int join_running_game(Smem<G>& sm, const EngineArrays& E, int games, int hint) {
+  if (wave_id() == 0) {
+    const int lane = lane_id_local();
+    unsigned best = 0xFFFFFFFFu;
+    int pick = -1;
+    for (int k0 = 1; k0 <= games; k0 += 64) {
+      const int k = k0 + lane;
+      const int t = (hint + k) % games;
+      unsigned key = 0xFFFFFFFFu;
+      if (k <= games) {
+        const JobView Jt = job_of<G>(E, t);
+        if (__hip_atomic_load(Jt.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kJobExit)
+          key = __hip_atomic_load(Jt.nhelp(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // (helpers, distance) lexicographic: the fewest helpers, then the nearest
+      unsigned long long v = (unsigned long long)key << 32 | (unsigned)k;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o);
+        v = w < v ? w : v;
+      }
+      if ((unsigned)(v >> 32) < best) { best = (unsigned)(v >> 32); pick = (hint + (int)(v & 0xFFFFFFFFu)) % games; }
+    }
+    if (lane == 0) {
+      if (pick >= 0) __hip_atomic_fetch_add(job_of<G>(E, pick).nhelp(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm.bc[2] = pick;
+    }
+  }
+  __syncthreads();
+  const int t = sm.bc[2];
+  __syncthreads();
+  return t;
+}
+
 // The simulations of one search with the tree accessor Acc (LDS or HBM stats).
 //
 // Factored dynamics also batch SPECULATIVELY: once a simulation's select ends
@@ -2043,7 +2084,7 @@ __device__ __forceinline__ void settle_all_priors(Smem<G>& sm, const TreeView& T
 }
 
 template <int N, int C>
-__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_search(NetParams np, SearchParams sp, EngineArrays E,
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_search(NetParams np_arg, SearchParams sp, EngineArrays E_arg,
                                                       const float* __restrict__ root_obs,
                                                       const double* __restrict__ noise, int game_base,
                                                       int move_index, int* out_visits, double* out_value) {
@@ -2051,6 +2092,10 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   __shared__ Smem<G> sm;
   static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
+  // (as k_selfplay_move: no address arithmetic hoisted into registers kept
+  // live across the whole search -- it spilled, 68 B/lane at 19x19)
+  const EngineArrays E = launder_arrays(E_arg);
+  const NetParams np = launder_params(np_arg);
   const int g = blockIdx.x;
   const float* o = root_obs + (size_t)g * 6 * G::CELLS;
   const uint64_t key = stream_key(sp.seed, (uint32_t)(game_base + g), (uint32_t)move_index);
@@ -2334,7 +2379,13 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if ((int)blockIdx.x >= games) {
     if constexpr (Smem<G>::GLOBAL_Y && G::WINO) {
       wino_raw_zero<G>(sm.raw);                          // the conv strips' zero halo
-      helper_loop<G>(sm, np_a_arg, np_b_arg, sp, E_arg, (blockIdx.x - games) % games);
+      int t = (blockIdx.x - games) % games;
+      for (;;) {
+        helper_loop<G>(sm, np_a_arg, np_b_arg, sp, E_arg, t);
+        if (!sp.tail) break;
+        t = join_running_game<G>(sm, E_arg, games, t);   // its game ended: the epoch tail
+        if (t < 0) break;
+      }
     }
     return;
   }
@@ -2344,8 +2395,16 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     if ((sp.helpers > 0 || sp.tail) && tid_local() == 0)
       __hip_atomic_store(job_of<G>(E_arg, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  // an ended game's workgroup serves running games' parent convs (9x9 epoch tail)
+  // an ended game's workgroup serves running games: their parent convs (9x9)
+  // or all their jobs as one more helper (19x19)
   auto tail_phase = [&]() {
+    if constexpr (Smem<G>::GLOBAL_Y && G::WINO) {
+      if (sp.tail) {
+        __syncthreads();
+        for (int t = g; (t = join_running_game<G>(sm, E_arg, games, t)) >= 0;)
+          helper_loop<G>(sm, np_a_arg, np_b_arg, sp, E_arg, t);
+      }
+    }
     if constexpr (TailConvs<G>::value)
       if (sp.tail) {
         __syncthreads();
