@@ -149,9 +149,16 @@ def phases_summary(workload, moves_per_launch):
     p = json.load(open(path))
     if p.get("workload") != workload:
         return None
-    return {"shares": {k: round(v, 4) for k, v in p["shares"].items()},
-            "tail_idle_cu_share": round(p["tail"]["idle_cu_share"], 4),
-            "source": f"profiles/{p['tag']}_phases.json"}
+    out = {"shares": {k: round(v, 4) for k, v in p["shares"].items()},
+           "tail_idle_cu_share": round(p["tail"]["idle_cu_share"], 4),
+           "source": f"profiles/{p['tag']}_phases.json"}
+    th = p.get("tail_helpers")
+    if th:
+        # ended games' workgroups computing running games' parent convs count as busy
+        out["tail_idle_cu_share_with_helpers"] = round(th["idle_cu_share_with_helpers"], 4)
+        out["tail_convs_share"] = round(p["engine_counters"]["tail_convs"] /
+                                        max(1, p["engine_counters"]["dynamics_convs"]), 4)
+    return out
 
 
 def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch):
@@ -373,6 +380,11 @@ def refill_main(args, net, world, rank, local, cpu_ref):
     = all simulations / wall time."""
     import mzgo
     N, C, S, G, R = args.board_size, args.latent_dim, args.sims, args.games, args.refill
+    # the epoch tail's helpers keep a finished game's workgroup on its CU (it
+    # serves running games' convs), which is exactly the CU the next engine's
+    # epoch would start on: refill and tail helpers exclude each other
+    # (same-call A/B: 106.2 M with them off, 95.6 M on)
+    os.environ["MZGO_TAIL_HELPERS"] = "0"
     sps = [mzgo.SelfPlay(net, G, S, seed=1234, game_base=(rank * R + r) * G, dynamics=args.dynamics)
            for r in range(R)]
     M = sps[0].max_moves
