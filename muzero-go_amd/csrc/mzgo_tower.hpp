@@ -914,13 +914,38 @@ __device__ __forceinline__ void tload_mask(TreeLds<G>& t, const TowerArrays& T, 
 }
 
 // sum of a board's head partials over the cout chunks (ascending) -> hp [3][CS]
+// (up to 4 chunks, C <= 256: every load of the wave issued before the first
+// add -- one memory round trip instead of one per 64 entries; the sums keep
+// the ascending chunk order)
 template <class G>
 __device__ __forceinline__ void tsum_heads(const TowerArrays& T, int b, float* hp) {
   const float* src = T.hpart + (size_t)b * T.co_chunks * 3 * G::CS;
-  for (int i = threadIdx.x; i < 3 * G::CS; i += 64) {
-    float s = src[i];
-    for (int c = 1; c < T.co_chunks; ++c) s += src[(size_t)c * 3 * G::CS + i];
-    hp[i] = s;
+  constexpr int PER = (3 * G::CS + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  if (T.co_chunks <= 4) {
+    float v[4][PER];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int i = lane + 64 * p;
+        v[c][p] = (c < T.co_chunks && i < 3 * G::CS) ? src[(size_t)c * 3 * G::CS + i] : 0.f;
+      }
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      const int i = lane + 64 * p;
+      float s = v[0][p];
+#pragma unroll
+      for (int c = 1; c < 4; ++c)
+        if (c < T.co_chunks) s += v[c][p];
+      if (i < 3 * G::CS) hp[i] = s;
+    }
+  } else {
+    for (int i = lane; i < 3 * G::CS; i += 64) {
+      float s = src[i];
+      for (int c = 1; c < T.co_chunks; ++c) s += src[(size_t)c * 3 * G::CS + i];
+      hp[i] = s;
+    }
   }
   wave_lds_sync();
 }
