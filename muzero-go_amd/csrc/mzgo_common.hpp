@@ -330,9 +330,14 @@ __device__ __forceinline__ T np_pairwise_sum(const T* x) {
     const int j = lane_id() & 7;
     T r = x[j];
     for (int i = 8; i < STOP; i += 8) r = r + x[i + j];
-    T r0 = dpp::lane(r, 0), r1 = dpp::lane(r, 1), r2 = dpp::lane(r, 2), r3 = dpp::lane(r, 3);
-    T r4 = dpp::lane(r, 4), r5 = dpp::lane(r, 5), r6 = dpp::lane(r, 6), r7 = dpp::lane(r, 7);
-    T res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) of the 8 partials in
+    // lanes 8k + j, by DPP within each 8-lane group (IEEE addition is
+    // commutative, so a lane's b + a equals its partner's a + b bit for bit):
+    // xor 1 pairs, xor 2 quads, half-row mirror (lane i <-> 7 - i) halves --
+    // every lane ends with the sum, no readlane
+    r = r + dpp::mov<dpp::XOR1>(r);
+    r = r + dpp::mov<dpp::XOR2>(r);
+    T res = r + dpp::mov<0x141>(r);
 #pragma unroll
     for (int i = STOP; i < N; ++i) res = res + x[i];
     return res;
