@@ -241,6 +241,13 @@ struct ExpandPlan {
 // same address), so no lane is masked off; the last pass's cells past the
 // board land in the row padding and stay out of S.  Wave-level; the caller
 // orders xw for the wave's readers (wave_lds_sync).
+// GLOBAL_Y boards: Y loads one pass pair ahead (MZGO_NO_EXPAND_PREFETCH for
+// the A/B build without; the same values either way)
+#ifdef MZGO_NO_EXPAND_PREFETCH
+constexpr bool kExpandPrefetch = false;
+#else
+constexpr bool kExpandPrefetch = true;
+#endif
 template <class G, int PROW>
 __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw,
                                             const ExpandPlan<G>& plan, float& rsum, float& vsum) {
@@ -263,6 +270,29 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   // every pass unrolled on small boards; two at a time on 19x19 (46 passes)
   // one pass: cells cg + 8 p, E rows at byte offset eoff of ew (LAST: the
   // final pass, whose cells past the board stay out of the sums)
+  // one pass over Y values already in registers
+  auto pass_y = [&](int p, const f32x4 (&y)[X::PERL], uint32_t eoff, bool last) {
+    const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + eoff);
+    f32x4 e[X::PERL];
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) e[k] = E4[8 * k];
+    const bool live = G::CELLS % 8 == 0 || !last || cg + 8 * p < G::CELLS;
+    f32x2 hp2 = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) {
+#pragma unroll
+      for (int q = 0; q < 4; q += 2) {
+        f32x2 v = f32x2{y[k][q], y[k][q + 1]} + f32x2{e[k][q], e[k][q + 1]};
+        v.x = v.x > 0.f ? v.x : 0.f;
+        v.y = v.y > 0.f ? v.y : 0.f;
+        hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
+        if (!live) v = f32x2{0.f, 0.f};
+        s2[k][q >> 1] = s2[k][q >> 1] + v;
+      }
+    }
+    xr[8 * p] = sum8(hp2.x + hp2.y);
+  };
+  (void)pass_y;
   auto pass = [&](int p, uint32_t eoff, bool last) {
     const f32x4* E4 = reinterpret_cast<const f32x4*>(Eb + eoff);
     f32x4 y[X::PERL], e[X::PERL];
@@ -295,6 +325,25 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
     // every pass unrolled, offsets from the plan's registers
 #pragma unroll
     for (int p = 0; p < P; ++p) pass(p, (plan.off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu, p == P - 1);
+  } else if constexpr (kExpandPrefetch) {
+    // pass pairs, one LDS table read per pair (19x19: 23 pairs), Y streamed
+    // from L2 one pass ahead: pass p + 1's loads are in flight while pass p
+    // is computed (each wave's passes are latency-bound on L2)
+    static_assert(P % 2 == 0, "whole pass pairs");
+    f32x4 ya[X::PERL], yb[X::PERL];
+    auto ldy = [&](int p, f32x4 (&y)[X::PERL]) {
+#pragma unroll
+      for (int k = 0; k < X::PERL; ++k) y[k] = Y4[p * 8 * X::C4 + 8 * k];
+    };
+    ldy(0, ya);
+#pragma unroll 1
+    for (int pp = 0; pp < P / 2; ++pp) {
+      const uint32_t w2 = plan.pair(pp, cg);
+      ldy(2 * pp + 1, yb);
+      pass_y(2 * pp, ya, w2 & 0xFFFFu, false);
+      if (pp + 1 < P / 2) ldy(2 * pp + 2, ya);
+      pass_y(2 * pp + 1, yb, w2 >> 16, pp + 1 == P / 2);
+    }
   } else {
     // pass pairs, one LDS table read per pair (19x19: 23 pairs); the last
     // pair (whose second pass holds the board's last cells) peeled off
