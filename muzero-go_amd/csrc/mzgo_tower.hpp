@@ -22,9 +22,9 @@
 // Activations (bf16) are stored per board as [C/64 chunks][P][64], P = (N+2)^2
 // padded pixels with a zero border (the conv's zero padding, never written),
 // each pixel's 128-byte row of 64 channels in 8 pieces of 16 bytes, piece j
-// at position j ^ ((q >> 1) & 7) (q = padded pixel index): the LDS image of a
+// at position j ^ tswz(q) (q = padded pixel index): the LDS image of a
 // chunk is a straight copy (global_load_lds) and the A-fragment reads of 16
-// consecutive pixels are bank-conflict free.  Weights are packed the same way
+// consecutive pixels are bank-conflict free (tswz below).  Weights are packed the same way
 // per (cout chunk, cin chunk, tap): [64 cout rows][64 cin], piece swizzled by
 // row.
 #pragma once
@@ -102,8 +102,33 @@ __device__ __forceinline__ int tcell(int m) {
   }
 }
 
+// The position of 16-byte piece j of padded pixel q's 128-byte row is
+// j ^ tswz(q).  A ds_read_b128 serves a wave in 4 lane groups of 16
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same +32: one LDS cycle
+// each when its 16 reads hit 16 distinct 16-byte bank slots); a group holds
+// MFMA rows 0-3 and 12-15 of one k piece and rows 4-11 of its neighbour
+// piece.  The slot of (q, j) is 8 (q & 1) + (j ^ tswz(q)), and with tswz(q)
+// = 2 ((q >> 1) & 3) any 16 consecutive pixels fill the 16 slots for every
+// piece pair (the even and the odd pixels each cover the 4 values of
+// (q >> 1) & 3 once in the rows the group reads at piece j and once at
+// j ^ 1, where the XOR moves them to the odd slot values).  Tiles of 16
+// pixels of one board row (kTowerRowSegments) are consecutive for every tap;
+// simulated over the 19x19 conv's fragment reads: 1.13 LDS cycles per lane
+// group (the 3-column tail tiles step by W), against 1.89 for (q >> 1) & 7
+// on raster tiles.  Measured (MZGO_TOWER_SWZ=1 MZGO_TOWER_ROWSEG=1, config
+// 5, rocprofv3): SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.326 -> 0.064,
+// LDS-array cycles -28 %, and k_tconv_ks no faster (25.8-26.0 vs 25.7 us,
+// same call): the fragment reads' conflicts are off the critical path.  The
+// default stays (q >> 1) & 7 on raster tiles, the faster of the two.
+#ifndef MZGO_TOWER_SWZ
+#define MZGO_TOWER_SWZ 0
+#endif
+__device__ __forceinline__ int tswz(int q) {
+  if constexpr (MZGO_TOWER_SWZ != 0) return ((q >> 1) & 3) << 1;
+  else return (q >> 1) & 7;
+}
 // element offset of (padded pixel q, channel c) inside one 64-channel chunk
-__device__ __forceinline__ int tpix(int q, int piece) { return q * 64 + ((piece ^ ((q >> 1) & 7)) << 3); }
+__device__ __forceinline__ int tpix(int q, int piece) { return q * 64 + ((piece ^ tswz(q)) << 3); }
 
 // ---------------------------------------------------------------------------
 // One 3x3 conv (+ bias [+ E-table term] [+ residual], ReLU) for nboards
@@ -267,7 +292,7 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
     // A fragments of group g (tap kx, tile i) of kernel row ky
     auto frag_a = [&](int kyv, int kx, int i, bf16x8 (&d)[2]) {
       const int q = qb[i] + kyv * G::W + kx;
-      const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
+      const int off = q * 128 + (((lane >> 4) ^ tswz(q)) << 4);
       d[0] = frag_ld(pbuf + off);
       d[1] = frag_ld(pbuf + (off ^ 64));
     };
@@ -324,7 +349,7 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
       auto load_a = [&](auto gc) {
         constexpr int g = decltype(gc)::value, kx = g / T::MT, i = g % T::MT;
         const int q = qb[i] + ky * G::W + kx;
-        const int off = q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4);
+        const int off = q * 128 + (((lane >> 4) ^ tswz(q)) << 4);
         af[g % (AD + 1)][0] = frag_ld(pbuf + off);
         af[g % (AD + 1)][1] = frag_ld(pbuf + (off ^ 64));
       };
@@ -627,7 +652,7 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
     bf16x8 afn[AD];
     auto frag_a = [&](int kyv, int kx, int i) {
       const int q = qb[i] + kyv * G::W + kx;
-      return frag_ld(pbuf + ((q * 128 + (((lane >> 4) ^ ((q >> 1) & 7)) << 4)) ^ hx));
+      return frag_ld(pbuf + ((q * 128 + (((lane >> 4) ^ tswz(q)) << 4)) ^ hx));
     };
     auto step = [&](auto kyc) {
       constexpr int ky = decltype(kyc)::value;
