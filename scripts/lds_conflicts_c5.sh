@@ -1,12 +1,13 @@
 #!/bin/bash
-# LDS bank conflicts of k_tconv_ks (config 5) for the default build and a
-# variant (libmzgo_oldswz.so, scripts/build_variant.sh): one --pmc pass each.
-# -> profiles/r4m_c5_lds_conflicts.txt
+# LDS bank conflicts of k_tconv_ks (config 5, 64 simulations) for library
+# builds, one --pmc pass each (profiles/r4m_c5_lds_conflicts.txt):
+#   LIBS="'' _swz" bash scripts/lds_conflicts_c5.sh
+# '' = muzero-go_amd/mzgo/libmzgo.so, _x = libmzgo_x.so (scripts/build_variant.sh)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
-for v in oldswz new; do
-  if [ $v = new ]; then L=muzero-go_amd/mzgo/libmzgo.so; else L=muzero-go_amd/mzgo/libmzgo_$v.so; fi
-  MZGO_LIB=$L timeout -s KILL 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/p2_$v -o run -- python3 bench.py --config 5 --sims 64 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/p2_$v.log 2>&1 || exit 1
-  python3 - $v <<'PY'
+eval "LIBA=(${LIBS:-''})"
+for v in "${LIBA[@]}"; do
+  MZGO_LIB=muzero-go_amd/mzgo/libmzgo$v.so timeout -s KILL 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/p2_lib$v -o run -- python3 bench.py --config 5 --sims 64 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/p2_lib$v.log 2>&1 || exit 1
+  python3 - "lib$v" <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(f"gpurun_out/p2_{sys.argv[1]}/**/*counter_collection.csv", recursive=True)[0]
 acc = collections.defaultdict(float); n = collections.Counter()
