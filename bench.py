@@ -248,19 +248,25 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, towers, towers_run):
     alg = boards * 2 * N * N * 9 * C * C
     exe = boards * 2 * 16 * ((N * N + 15) // 16) * 9 * C * C
     ach = alg / avg_launch_s / 1e12
-    kname = "k_tconv" if os.environ.get("MZGO_TCONV_KS") == "0" else "k_tconv_ks"
+    # one k_tconv_chain launch per tower (all L convs) unless MZGO_TCONV_CHAIN=0
+    chain = os.environ.get("MZGO_TCONV_CHAIN") != "0" and G * (C // 64) <= 256
+    kname = "k_tconv_chain" if chain else ("k_tconv" if os.environ.get("MZGO_TCONV_KS") == "0" else "k_tconv_ks")
     out = {"bound": "mfma", "kernel": f"{kname}<{N}>", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS,
            "unit": "TFLOP/s", "frac": ach / PEAK_BF16_MFMA_TFLOPS, "traffic": None,
            "avg_launch_ms": avg_launch_s * 1e3, "launches_per_simulation": L, "boards_per_launch": boards,
            "flops_per_launch": alg, "executed_flops_per_launch": exe,
            "mfma_executed_tflops": exe / avg_launch_s / 1e12,
-           "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board) / average k_tconv launch time "
-                   "(HIP events around every 16th simulation's tower / its launches, gaps included)"}
+           "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board) / average time per conv "
+                   "(HIP events around every 16th simulation's tower / its L convs, gaps included; "
+                   "k_tconv_chain runs a tower's L convs in one launch, so its per-launch counters are / L)"}
+    if chain:
+        out["convs_per_launch"] = L
     path = os.path.join(ROOT, "profiles", "latest_tower_pmc.json")
     if os.path.exists(path):
         p = json.load(open(path))
-        if p.get("workload") == f"{N}x{N}/C{C}/B{blocks}/G{G}":
-            out["traffic"] = p.get("hbm_bytes_per_launch")
+        if p.get("workload") == f"{N}x{N}/C{C}/B{blocks}/G{G}" and ("chain" in p.get("kernel", "")) == chain:
+            per = L if chain else 1                     # (the chain's counters cover L convs)
+            out["traffic"] = p.get("hbm_bytes_per_launch") / per if p.get("hbm_bytes_per_launch") else None
             out["pmc_source"] = f"profiles/{p['tag']}_pmc.json"
             out["pmc"] = p.get("derived")
             clk = (p.get("derived") or {}).get("in_kernel_clock_GHz")
@@ -351,7 +357,7 @@ def tower_main(args, world, rank, local, cpu_ref):
             "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
             "moves_per_s": moves / dt,
             "config": {"workload": workload, "step": f"one move of {G} games/GPU ({S} simulations each; "
-                                                     f"{2 * B + 1} k_tconv launches per simulation)"
+                                                     f"{2 * B + 1} convs per simulation)"
                                                      + (f", from move {args.start_move}" if args.start_move else ""),
                        "board_size": N, "latent_dim": C, "res_blocks": B, "games_per_gpu": G,
                        "sims_per_move": S, "parallelism": f"game-sharded x{world}", "compat": "reference",

@@ -219,6 +219,7 @@ struct mzgo_engine {
   ~mzgo_engine() {
     if (tower) {
       for (hipEvent_t ev : tower->evs) (void)hipEventDestroy(ev);
+      tower->free_chains();
       for (void* p : {tower->d_wb, (void*)tower->d_wf, (void*)tower->ib, (void*)tower->ob, (void*)tower->s0,
                       (void*)tower->s1, (void*)tower->shp, (void*)tower->sact})
         if (p) (void)hipFree(p);
@@ -724,6 +725,9 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
       if (k > 0 && k % 4 == 0) {
         HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        bool bad = false;
+        HIPCHK(t.chain_error(s, bad));
+        if (bad) return fail(MZGO_EHIP, "k_tconv_chain: a workgroup's wait for its board expired");
         bool any = false;
         for (int v : st) any |= v == 0;
         if (!any) break;

@@ -550,13 +550,55 @@ struct TConvKsGeo {
   static_assert(8 * MT * 2 * 1024 <= 2 * T::PB + 2 * T::WSLOT, "the epilogue's accumulator exchange fits the patch buffers + ring");
 };
 
+// workgroup -> (board, cout chunk): with nboards % 8 == 0 a board's CO
+// workgroups are bid = x + 8 (j CO + cg) (board x + 8 j), all on XCD x (the
+// dispatcher deals workgroups to the 8 XCDs in turn), so a board's chunks
+// stay in one L2 from conv to conv
+__device__ __forceinline__ void tconv_slot(int nboards, int CO, int& b, int& cg) {
+  const int bid = blockIdx.x;
+  if (nboards % 8 == 0) {
+    const int x = bid & 7, k = bid >> 3;
+    b = x + 8 * (k / CO);
+    cg = k % CO;
+  } else {
+    b = bid / CO;
+    cg = bid % CO;
+  }
+}
+
+// This workgroup's (board, cout chunk) of conv a (tconv_slot; the body of
+// k_tconv_ks and of each layer of k_tconv_chain).  All threads.
+// the conv's LDS (patch buffers, weight ring, bias / head weights)
 template <int N>
-__global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
+__device__ __forceinline__ char* tconv_lds() {
+  __shared__ __attribute__((aligned(16))) char lds[TConvGeo<N, 8>::LDS];
+  return lds;
+}
+
+// step 0's weight tile of conv a into ring slot 0 (k_tconv_chain issues it
+// for the next layer before it waits for the board: slot 0 is free from
+// the previous conv's last step on).  All threads.
+template <int N>
+__device__ __forceinline__ void tconv_issue_w0(const TConvArgs& a, int cg) {
+  typedef TConvGeo<N, 8> T;
+  char* const slot = tconv_lds<N>() + 2 * T::PB;
+  const char* src = reinterpret_cast<const char*>(a.w + (size_t)cg * a.ci_chunks * 9 * 64 * 64);
+  const int wave = __builtin_amdgcn_readfirstlane(tid_local() >> 6), lane = tid_local() & 63;
+#pragma unroll
+  for (int k = 0; k < T::WPW; ++k) {
+    const int ii = k * 8 + wave;
+    dma16(src + ii * 1024 + lane * 16, lds_addr(slot + ii * 1024));
+  }
+}
+
+// w0_issued: tconv_issue_w0 ran for this conv already
+template <int N>
+__device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issued = false) {
   typedef TGeo<N> G;
   typedef TConvGeo<N, 8> T;
   typedef TConvKsGeo<N> K;
   constexpr int NW = 8, MT = K::MT, AD = K::ADIST, NG = 3 * MT;
-  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+  char* const lds = tconv_lds<N>();
   STAMP_T(tstart);
 #ifdef MZGO_TCONV_STAMPS
   unsigned long long acc_wait = 0, acc_bar = 0, acc_mfma = 0;
@@ -565,16 +607,8 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
   const int CO = a.co_chunks, CC = a.ci_chunks;
   const int bid = blockIdx.x;
   int b, cg;
-  if (a.nboards % 8 == 0) {
-    const int x = bid & 7, k = bid >> 3;
-    b = x + 8 * (k / CO);
-    cg = k % CO;
-  } else {
-    b = bid / CO;
-    cg = bid % CO;
-  }
-  if (a.active && !a.active[b]) return;
-  const int tid = threadIdx.x, lane = tid & 63;
+  tconv_slot(a.nboards, CO, b, cg);
+  const int tid = tid_local(), lane = tid & 63;   // (tid_local: nothing lane-derived is hoisted out of k_tconv_chain's layer loop)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = wave >> 2, mg = wave & 3;
   if constexpr (kPrio == 2)
@@ -612,7 +646,7 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
   };
   const int nsteps = 3 * CC;
   issue_patch_pieces(0, 0, 0, T::NPW);
-  issue_w(0);
+  if (!w0_issued) issue_w(0);
 
   // this wave's half of a 64-channel row: byte 64 * kh of the pixel's 128
   const int hx = kh * 64;
@@ -901,6 +935,119 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
     g[5] += tend - tloop; g[6] += 1; g[7] += txch - tloop;
   }
 #endif
+}
+
+template <int N>
+__global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
+  int b, cg;
+  tconv_slot(a.nboards, a.co_chunks, b, cg);
+  if (a.active && !a.active[b]) return;
+  tconv_ks_board<N>(a);
+}
+
+// ---------------------------------------------------------------------------
+// k_tconv_chain: the nl convs of one tower (layers[0..nl), each a
+// k_tconv_ks conv) in ONE launch.  Workgroup (b, cg) computes cout chunk cg
+// of board b for every layer in turn; layer l + 1 reads all CO chunks of
+// board b's layer-l output (and a residual it wrote itself earlier), so
+// before it starts, the workgroup waits until the board's CO workgroups
+// have published layer l: flags[b * CO + k] = seq0 + l + 1 (monotonic
+// across launches; compared modulo 2^32).  A board's workgroups only wait on
+// each other, and the launch has at most one workgroup per CU (T::LDS), so
+// the host uses it only when all nboards * CO workgroups fit the chip at
+// once; every wait is bounded (~1 s): on expiry *err is set and the
+// workgroup stops waiting (wrong results, reported, never a hung GPU).
+//
+// Hand-off.  Agent scope (cdna_hip_programming.md G16: drained stores, a
+// barrier, buffer_wbl2 + flag; flag, buffer_inv sc1) writes back and
+// invalidates the XCD's L2 per workgroup and layer, so every later read of
+// the weights misses L2 -- measured 14 % slower than one launch per conv.
+// Each workgroup therefore first publishes its XCC id (HW_REG_XCC_ID); when
+// all CO workgroups of its board run on one XCC (the usual placement,
+// tconv_slot) the board's hand-offs stay inside that XCC's L2, the
+// coherence point of its CUs: the producer drains its stores to L2 and
+// stores the flag, the consumer sees the flag and invalidates only its CU's
+// L1 (buffer_inv sc0).  A board split over XCCs keeps the agent-scope
+// protocol.  Replaces 2 blocks + 1 launches per tower: no per-launch
+// dispatch ramp and drain, and a board starts its next conv as soon as its
+// own chunks are done.
+// ---------------------------------------------------------------------------
+struct TConvChain {
+  const TConvArgs* layers;   // [nl] (device memory)
+  int nl;
+  unsigned* flags;           // [nboards * co_chunks]: layers published
+  unsigned long long* xcc;   // [nboards * co_chunks]: seq0 << 32 | XCC id of the launch
+  unsigned seq0;
+  int* err;
+};
+
+// bounded wait until (int)(*p - want) >= 0 (thread 0); false on expiry
+__device__ __forceinline__ bool chain_wait(const unsigned* p, unsigned want) {
+  for (long long spins = 0; (int)(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0;
+       ++spins) {
+    if (spins > (1ll << 24)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+template <int N>
+__global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c) {
+  __shared__ int s_local;
+  const int nboards = c.layers[0].nboards, CO = c.layers[0].co_chunks;
+  int b, cg;
+  tconv_slot(nboards, CO, b, cg);
+  const int* active = c.layers[0].active;
+  if (active && !active[b]) return;
+  unsigned* fl = c.flags + (size_t)b * CO;
+  bool bad = false;
+  // this launch's placement: is every chunk of board b on this XCC?
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    x &= 0xFu;
+    unsigned long long* xs = c.xcc + (size_t)b * CO;
+    __hip_atomic_store(xs + cg, (unsigned long long)c.seq0 << 32 | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int local = 1;
+    for (int k = 0; k < CO; ++k) {
+      unsigned long long v = __hip_atomic_load(xs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (long long spins = 0; (unsigned)(v >> 32) != c.seq0; ++spins) {
+        if (spins > (1ll << 24)) { bad = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(xs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (bad) break;
+      local &= (unsigned)(v & 0xFu) == x ? 1 : 0;
+    }
+    if (bad) atomicOr(c.err, 2);
+    s_local = bad ? 0 : local;
+  }
+  __syncthreads();
+  const bool local = s_local != 0;
+  for (int l = 0; l < c.nl; ++l) {
+    if (l > 0) {
+      // lanes 0..CO-1 of wave 0 poll the board's CO flags at once (one round trip each)
+      if (threadIdx.x < (unsigned)CO && !bad) {
+        if (!chain_wait(fl + threadIdx.x, c.seq0 + (unsigned)l)) {
+          atomicOr(c.err, 1);
+          bad = true;
+        }
+        if (local) asm volatile("buffer_inv sc0" ::: "memory");   // this CU's L1 (the data is in the XCC's L2)
+        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      __syncthreads();
+    }
+    const TConvArgs& a = c.layers[l];   // (fields read where used: fewer live SGPRs)
+    tconv_ks_board<N>(a, l > 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (!local) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(fl + cg, c.seq0 + (unsigned)l + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the next conv's first weight tile lands while the board's other chunks finish
+    if (l + 1 < c.nl) tconv_issue_w0<N>(c.layers[l + 1], cg);
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -13,6 +13,7 @@ hipError_t launch_tact(const int64_t* a, int* out, int B, int A, int* err, hipSt
 struct TowerSet {
   int N;
   hipError_t (*conv)(const TConvArgs&, hipStream_t);
+  hipError_t (*chain)(const TConvChain&, int workgroups, hipStream_t);
   hipError_t (*obs)(const TowerArrays&, const SearchParams&, const PlayParams&, const EngineArrays&, int G,
                     hipStream_t);
   hipError_t (*obs_search)(const TowerArrays&, const SearchParams&, const float* obs, int game_base, int move,
@@ -49,6 +50,10 @@ struct TLaunch {
       hipLaunchKernelGGL((k_tconv<N, 4>), dim3(a.nboards * a.co_chunks), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((k_tconv<N, 8>), dim3(a.nboards * a.co_chunks), dim3(512), 0, s, a);
+    return hipGetLastError();
+  }
+  static hipError_t chain(const TConvChain& c, int workgroups, hipStream_t s) {
+    hipLaunchKernelGGL((k_tconv_chain<N>), dim3(workgroups), dim3(512), 0, s, c);
     return hipGetLastError();
   }
   static hipError_t obs(const TowerArrays& T, const SearchParams& sp, const PlayParams& pp, const EngineArrays& E,
@@ -100,7 +105,7 @@ struct TLaunch {
     return hipGetLastError();
   }
   static TowerSet table() {
-    return TowerSet{N, &conv, &obs, &obs_search, &root, &select, &expand, &choose, &search_out, &tin, &tout,
+    return TowerSet{N, &conv, &chain, &obs, &obs_search, &root, &select, &expand, &choose, &search_out, &tin, &tout,
                     &theads};
   }
 };

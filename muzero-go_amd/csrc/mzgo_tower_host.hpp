@@ -77,6 +77,90 @@ struct TowerHost {
 
   long long slot() const { return (long long)CC * P * 64; }
 
+  // k_tconv_chain: a tower's convs in one launch when all of its nb x CC
+  // workgroups (one per CU) are resident at once; MZGO_TCONV_CHAIN=0 keeps
+  // one k_tconv_ks launch per conv.  The layer tables live on the device,
+  // one per distinct tower call (the dynamics tower's is the same every
+  // simulation); the per-(board, cout chunk) flags count layers done.
+  int ncu = -1;
+  unsigned* cflags = nullptr; int cflags_n = 0;
+  unsigned long long* cxcc = nullptr;
+  int* cerr = nullptr;
+  unsigned cseq = 0;
+  struct ChainBuf { std::vector<TConvArgs> host; TConvArgs* dev = nullptr; };
+  std::vector<ChainBuf> chains;
+  bool chain_ok(int nb) {
+    static const bool on = [] { const char* e = getenv("MZGO_TCONV_CHAIN"); return !(e && atoi(e) == 0); }();
+    if (!on || !ts->chain) return false;
+    if (ncu < 0) {
+      int dev = 0;
+      ncu = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        ncu = 0;
+    }
+    return nb * CC <= ncu;
+  }
+  hipError_t launch_chain(const std::vector<TConvArgs>& L, int nb, hipStream_t s) {
+    hipError_t e;
+    if (cflags_n < nb * CC) {
+      if (cflags) (void)hipFree(cflags);
+      if (cxcc) (void)hipFree(cxcc);
+      cflags = nullptr;
+      cxcc = nullptr;
+      if ((e = hipMalloc(&cflags, (size_t)nb * CC * sizeof(unsigned))) != hipSuccess) return e;
+      if ((e = hipMemset(cflags, 0, (size_t)nb * CC * sizeof(unsigned))) != hipSuccess) return e;
+      if ((e = hipMalloc(&cxcc, (size_t)nb * CC * sizeof(unsigned long long))) != hipSuccess) return e;
+      if ((e = hipMemset(cxcc, 0xFF, (size_t)nb * CC * sizeof(unsigned long long))) != hipSuccess) return e;
+      cflags_n = nb * CC;
+      cseq = 0;
+    }
+    if (!cerr) {
+      if ((e = hipMalloc(&cerr, sizeof(int))) != hipSuccess) return e;
+      if ((e = hipMemset(cerr, 0, sizeof(int))) != hipSuccess) return e;
+    }
+    const TConvArgs* dev = nullptr;
+    for (const ChainBuf& c : chains)
+      if (c.host.size() == L.size() && std::memcmp(c.host.data(), L.data(), L.size() * sizeof(TConvArgs)) == 0)
+        dev = c.dev;
+    if (!dev) {
+      ChainBuf c;
+      c.host = L;
+      if ((e = hipMalloc(&c.dev, L.size() * sizeof(TConvArgs))) != hipSuccess) return e;
+      if ((e = hipMemcpy(c.dev, L.data(), L.size() * sizeof(TConvArgs), hipMemcpyHostToDevice)) != hipSuccess) {
+        (void)hipFree(c.dev);
+        return e;
+      }
+      dev = c.dev;
+      chains.push_back(std::move(c));
+    }
+    const TConvChain ch{dev, (int)L.size(), cflags, cxcc, cseq, cerr};
+    cseq += (unsigned)L.size();
+    return ts->chain(ch, nb * CC, s);
+  }
+  // a chain wait expired (results of that launch are wrong): read at the
+  // host's synchronisation points
+  hipError_t chain_error(hipStream_t s, bool& bad) {
+    bad = false;
+    if (!cerr) return hipSuccess;
+    int v = 0;
+    hipError_t e = hipMemcpyAsync(&v, cerr, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    bad = v != 0;
+    return e;
+  }
+  void free_chains() {
+    for (ChainBuf& c : chains)
+      if (c.dev) (void)hipFree(c.dev);
+    chains.clear();
+    if (cflags) (void)hipFree(cflags);
+    if (cxcc) (void)hipFree(cxcc);
+    if (cerr) (void)hipFree(cerr);
+    cflags = nullptr;
+    cxcc = nullptr;
+    cerr = nullptr;
+  }
+
   hipError_t mark(hipStream_t s) {
     if (!timing) return hipSuccess;
     if (ev_used == evs.size()) {
@@ -221,13 +305,13 @@ struct TowerHost {
   // last block's into out) with the fused heads on the final conv.
   hipError_t tower(const std::vector<Conv>& L, const bf16* in, const int* in_idx, long long in_stride, bf16* out,
                    const int* out_idx, long long out_stride, const int* act, const int* active, int nb, bf16* a0,
-                   bf16* a1, float* hpart, hipStream_t s) const {
+                   bf16* a1, float* hpart, hipStream_t s) {
     TConvArgs c{};
     c.nboards = nb;
     c.co_chunks = CC;
     c.active = active;
     const long long sl = slot();
-    hipError_t e;
+    std::vector<TConvArgs> layers;
     auto run = [&](const Conv& cv, const bf16* src, const int* sidx, long long sstr, bf16* dst, const int* didx,
                    long long dstr, const bf16* res, bool heads, const float* et) {
       c.in = src; c.in_idx = sidx; c.in_stride = sstr;
@@ -236,25 +320,32 @@ struct TowerHost {
       c.w = cv.w; c.bias = cv.b; c.ci_chunks = cv.cin_chunks;
       c.etab = et; c.act = et ? act : nullptr;
       c.headw = heads ? TA.headw : nullptr; c.hpart = hpart;
-      return ts->conv(c, s);
+      layers.push_back(c);
     };
     const int nb_ = (int)(L.size() - 1) / 2;
     const float* et = act ? etab : nullptr;
-    if (nb_ == 0) return run(L[0], in, in_idx, in_stride, out, out_idx, out_stride, nullptr, true, et);
-    if ((e = run(L[0], in, in_idx, in_stride, a0, nullptr, sl, nullptr, false, et)) != hipSuccess) return e;
-    for (int k = 0; k < nb_; ++k) {
-      const bool lastb = k == nb_ - 1;
-      if ((e = run(L[1 + 2 * k], a0, nullptr, sl, a1, nullptr, sl, nullptr, false, nullptr)) != hipSuccess) return e;
-      if ((e = run(L[2 + 2 * k], a1, nullptr, sl, lastb ? out : a0, lastb ? out_idx : nullptr,
-                   lastb ? out_stride : sl, a0, lastb, nullptr)) != hipSuccess)
-        return e;
+    if (nb_ == 0) {
+      run(L[0], in, in_idx, in_stride, out, out_idx, out_stride, nullptr, true, et);
+    } else {
+      run(L[0], in, in_idx, in_stride, a0, nullptr, sl, nullptr, false, et);
+      for (int k = 0; k < nb_; ++k) {
+        const bool lastb = k == nb_ - 1;
+        run(L[1 + 2 * k], a0, nullptr, sl, a1, nullptr, sl, nullptr, false, nullptr);
+        run(L[2 + 2 * k], a1, nullptr, sl, lastb ? out : a0, lastb ? out_idx : nullptr, lastb ? out_stride : sl, a0,
+            lastb, nullptr);
+      }
+    }
+    if (layers.size() > 1 && chain_ok(nb)) return launch_chain(layers, nb, s);
+    for (const TConvArgs& l : layers) {
+      hipError_t e = ts->conv(l, s);
+      if (e != hipSuccess) return e;
     }
     return hipSuccess;
   }
 
   // representation tower + root priors for the slots marked playing
   hipError_t root_phase(const SearchParams& sp, const EngineArrays& E, const double* noise, long long nstride,
-                        int per_move, hipStream_t s) const {
+                        int per_move, hipStream_t s) {
     hipError_t e;
     if ((e = tower(rep, TA.rep_in, nullptr, (long long)P * 64, TA.pool, TA.root_idx, slot(), nullptr, TA.playing, G,
                    t0, t1, TA.hpart, s)) != hipSuccess)

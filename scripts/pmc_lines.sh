@@ -15,7 +15,7 @@ for l in ${LINES:-head 9_400 refill2 19_64 c5}; do
     9_400)   A="--sims 400 --steps 1 --warmup 1 --no-cpu-baseline"; WL="$W9, 400 sims/move"; K=k_selfplay_move; F=latest_pmc_9x9_g256_s400.json ;;
     refill2) A="--refill 2 --steps 2 --warmup 2 --no-cpu-baseline"; WL="$W9, 200 sims/move, refill 2"; K=k_selfplay_move; F=latest_pmc_9x9_g256_s200_refill2.json ;;
     19_64)   A="--board-size 19 --games 64 --sims 800 --steps 1 --warmup 1 --no-cpu-baseline"; WL="19x19 Go self-play, 64 parallel games/GPU, 800 sims/move"; K=k_selfplay_move; F=latest_pmc_19x19_g64_s800.json ;;
-    c5)      A="--config 5 --sims 64 --steps 1 --warmup 1 --no-cpu-baseline"; WL="19x19/C256/B20/G64"; K=k_tconv_ks; F=latest_tower_pmc.json ;;
+    c5)      A="--config 5 --sims 64 --steps 1 --warmup 1 --no-cpu-baseline"; WL="19x19/C256/B20/G64"; K=k_tconv_chain; F=latest_tower_pmc.json ;;
     *) echo "unknown line $l" >&2; exit 2 ;;
   esac
   bash scripts/pmc.sh ${TAG}_$l $A > gpurun_out/pmc_${TAG}_$l.log 2>&1 || { tail -20 gpurun_out/pmc_${TAG}_$l.log; exit 1; }
