@@ -11,9 +11,10 @@
 //
 //   k_tselect   one wave per game: select_leaf (self_play.py:239-335) on the
 //               game's HBM tree -> (leaf latent slot, action, new node slot)
-//   k_tconv     x 41: the tower, ALL games' leaves in one launch per conv --
+//   k_tconv_chain: the tower's 41 convs, ALL games' leaves, in one launch --
 //               implicit GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16, fp32
-//               accumulate), one (board, 64-cout chunk) per workgroup
+//               accumulate), one (board, 64-cout chunk) per workgroup through
+//               every layer (k_tconv_ks: the same conv, one launch per layer)
 //   k_texpand   one wave per game: heads -> child priors, backup (:198-230)
 //
 // Each game contributes exactly one leaf per simulation step, so the batch
