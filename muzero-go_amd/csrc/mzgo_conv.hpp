@@ -289,6 +289,21 @@ __device__ __forceinline__ void dma16(const void* g, uint32_t lds_dst) {
 
 // 4 bytes per lane (LDS destination base + lane*4): an L2 prefetch whose data
 // lands in a dummy LDS area
+// dma16 with sc0: the read is served from L2, never from this CU's L1 (data
+// that other CUs of the XCC wrote since: k_tconv_chain's layer hand-offs)
+__device__ __forceinline__ void dma16_l2(const void* g, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off sc0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds_dst)
+      : "memory");
+}
+
 __device__ __forceinline__ void dma4(const void* g, uint32_t lds_dst) {
   uint32_t keep;
   asm volatile(

@@ -592,6 +592,20 @@ __device__ __forceinline__ void tconv_issue_w0(const TConvArgs& a, int cg) {
   }
 }
 
+// The patch pieces bypass L1 (dma16_l2): an input chunk is read once per
+// conv and workgroup, and in k_tconv_chain it was written by other CUs of
+// the XCC since the last read, so no L1 invalidate is needed between layers
+// (MZGO_TCONV_PATCH_L1=1: through L1, with buffer_inv sc0 per layer).
+#ifdef MZGO_TCONV_PATCH_L1
+constexpr bool kPatchL2 = false;
+#else
+constexpr bool kPatchL2 = true;
+#endif
+__device__ __forceinline__ void dma_patch(const void* g, uint32_t lds_dst) {
+  if constexpr (kPatchL2) dma16_l2(g, lds_dst);
+  else dma16(g, lds_dst);
+}
+
 // w0_issued: tconv_issue_w0 ran for this conv already
 template <int N>
 __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issued = false) {
@@ -633,7 +647,7 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
       const int ii = k * NW + wave;
       if (ii >= T::PPIECES) break;
       const int off = ii * 1024 + lane * 16;
-      if (off < T::PBYTES) dma16(src + off, lds_addr(patch0 + buf * T::PB + ii * 1024));
+      if (off < T::PBYTES) dma_patch(src + off, lds_addr(patch0 + buf * T::PB + ii * 1024));
     }
   };
   auto issue_w = [&](int s) {
@@ -730,7 +744,7 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
           const int ii = (PK0 + j - T::WPW) * NW + wave;
           const int off = ii * 1024 + lane * 16;
           if (ii < T::PPIECES && off < T::PBYTES)
-            dma16(reinterpret_cast<const char*>(in + (size_t)(cc + 1) * G::P * 64) + off,
+            dma_patch(reinterpret_cast<const char*>(in + (size_t)(cc + 1) * G::P * 64) + off,
                   lds_addr(patch0 + ((cc + 1) & 1) * T::PB + ii * 1024));
         }
       };
@@ -967,8 +981,8 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
 // all CO workgroups of its board run on one XCC (the usual placement,
 // tconv_slot) the board's hand-offs stay inside that XCC's L2, the
 // coherence point of its CUs: the producer drains its stores to L2 and
-// stores the flag, the consumer sees the flag and invalidates only its CU's
-// L1 (buffer_inv sc0).  A board split over XCCs keeps the agent-scope
+// stores the flag, the consumer sees the flag and reads the patch from L2
+// past its CU's L1 (dma_patch).  A board split over XCCs keeps the agent-scope
 // protocol.  Replaces 2 blocks + 1 launches per tower: no per-launch
 // dispatch ramp and drain, and a board starts its next conv as soon as its
 // own chunks are done.
@@ -1033,8 +1047,13 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c) {
           atomicOr(c.err, 1);
           bad = true;
         }
-        if (local) asm volatile("buffer_inv sc0" ::: "memory");   // this CU's L1 (the data is in the XCC's L2)
-        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // local: the data is in the XCC's L2, which the patch reads go to
+        // (dma_patch); otherwise this CU's L1 would be invalidated here
+        if (local) {
+          if constexpr (!kPatchL2) asm volatile("buffer_inv sc0" ::: "memory");
+        } else {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
       }
       __syncthreads();
     }
