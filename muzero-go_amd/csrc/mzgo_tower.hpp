@@ -1007,12 +1007,14 @@ __device__ __forceinline__ bool chain_wait(const unsigned* p, unsigned want) {
 }
 
 template <int N>
-__global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c) {
+__global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c, const TConvArgs* __restrict__ layers) {
+  // (layers: c.layers as a restrict pointer, so the fields are scalar loads
+  // -- read-only for the launch -- not vector loads in every epilogue)
   __shared__ int s_local;
-  const int nboards = c.layers[0].nboards, CO = c.layers[0].co_chunks;
+  const int nboards = layers[0].nboards, CO = layers[0].co_chunks;
   int b, cg;
   tconv_slot(nboards, CO, b, cg);
-  const int* active = c.layers[0].active;
+  const int* active = layers[0].active;
   if (active && !active[b]) return;
   unsigned* fl = c.flags + (size_t)b * CO;
   bool bad = false;
@@ -1057,7 +1059,7 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c) {
       }
       __syncthreads();
     }
-    const TConvArgs& a = c.layers[l];   // (fields read where used: fewer live SGPRs)
+    const TConvArgs& a = layers[l];   // (fields read where used: fewer live SGPRs)
     tconv_ks_board<N>(a, l > 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1066,7 +1068,7 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c) {
       __hip_atomic_store(fl + cg, c.seq0 + (unsigned)l + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the next conv's first weight tile lands while the board's other chunks finish
-    if (l + 1 < c.nl) tconv_issue_w0<N>(c.layers[l + 1], cg);
+    if (l + 1 < c.nl) tconv_issue_w0<N>(layers[l + 1], cg);
   }
 }
 

@@ -53,7 +53,7 @@ struct TLaunch {
     return hipGetLastError();
   }
   static hipError_t chain(const TConvChain& c, int workgroups, hipStream_t s) {
-    hipLaunchKernelGGL((k_tconv_chain<N>), dim3(workgroups), dim3(512), 0, s, c);
+    hipLaunchKernelGGL((k_tconv_chain<N>), dim3(workgroups), dim3(512), 0, s, c, c.layers);
     return hipGetLastError();
   }
   static hipError_t obs(const TowerArrays& T, const SearchParams& sp, const PlayParams& pp, const EngineArrays& E,
