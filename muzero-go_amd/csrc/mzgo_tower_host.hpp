@@ -90,8 +90,8 @@ struct TowerHost {
   struct ChainBuf { std::vector<TConvArgs> host; TConvArgs* dev = nullptr; };
   std::vector<ChainBuf> chains;
   bool chain_ok(int nb) {
-    static const bool on = [] { const char* e = getenv("MZGO_TCONV_CHAIN"); return !(e && atoi(e) == 0); }();
-    if (!on || !ts->chain) return false;
+    const char* env = getenv("MZGO_TCONV_CHAIN");                // (read per tower: tests switch it)
+    if ((env && atoi(env) == 0) || !ts->chain) return false;
     if (ncu < 0) {
       int dev = 0;
       ncu = 0;

@@ -343,3 +343,33 @@ def test_tower_multi_move_call_equals_single_moves():
         for k in ("stones", "invd", "flags", "action", "value", "policy", "reward"):
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
         assert a["final_reward"] == b["final_reward"]
+
+
+def test_tower_chain_launch_equals_per_conv_launches(monkeypatch):
+    """k_tconv_chain (a tower's convs in one launch, the boards' 4 cout-chunk
+    workgroups handing layers to each other through flags) against one
+    k_tconv_ks launch per conv (MZGO_TCONV_CHAIN=0): the same per-layer body,
+    so the same records and trees, byte for byte.  C = 128 (2 cout chunks:
+    the hand-offs cross workgroups), 2 blocks, 9x9, 8 games x 24 simulations
+    x 3 moves."""
+    import mzgo
+    N, C, blocks, G, S = 9, 128, 2, 8, 24
+    net = _nets(N, C, blocks, seed=5)[0]
+    out = []
+    for chain in ("1", "0"):
+        monkeypatch.setenv("MZGO_TCONV_CHAIN", chain)
+        sp = mzgo.SelfPlay(net, G, S, seed=11)
+        sp.reset()
+        sp.move(3)
+        torch.cuda.synchronize()
+        recs = [sp.engine.record(g) for g in range(G)]
+        trees = [sp.engine.tree(g) for g in range(2)]
+        out.append((recs, trees))
+    (ra, ta), (rb, tb) = out
+    for a, b in zip(ra, rb):
+        assert a.keys() == b.keys()
+        for k in a:
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    for a, b in zip(ta, tb):
+        for k in a:
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
