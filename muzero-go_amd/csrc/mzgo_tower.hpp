@@ -857,6 +857,7 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
   };
   if (kh == 0) give(std::integral_constant<int, 0>{});
   else give(std::integral_constant<int, 1>{});
+  STAMP_T(tgive);
   if (a.etab) {
     const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
     for (int k = tid; k < 9 * 64; k += NW * 64) set[k] = eb[(size_t)(k >> 6) * CO * 64 + (k & 63)];
@@ -926,6 +927,7 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
   };
   if (kh == 0) finish(std::integral_constant<int, 0>{});
   else finish(std::integral_constant<int, 1>{});
+  STAMP_T(tfin);
   // 3. kh = 0 stores the chunk's head partials
   if (a.headw) {
     __syncthreads();
@@ -948,6 +950,7 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
     g[8] += rend - rstart;
     g[0] += tend - tstart; g[1] += tpro - tstart; g[2] += acc_wait; g[3] += acc_bar; g[4] += acc_mfma;
     g[5] += tend - tloop; g[6] += 1; g[7] += txch - tloop;
+    g[9] += tgive - tloop; g[10] += tfin - tgive; g[11] += txch - tfin;
   }
 #endif
 }

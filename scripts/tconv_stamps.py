@@ -25,7 +25,8 @@ dt = time.perf_counter() - t0
 f(out)
 n = out[6]
 clk = [out[w * 16] / max(out[w * 16 + 8], 1) * 0.1 for w in range(8)]
-names = ["total", "prologue", "vmcnt waits", "barriers", "MFMA steps", "epilogue", "", "epi: exchange"]
+names = ["total", "prologue", "vmcnt waits", "barriers", "MFMA steps", "epilogue", "", "epi: exchange", "",
+         "epi: give", "epi: barrier + finish", "epi: heads"]
 print(f"workgroup-launches {n}, move {dt*1e3:.1f} ms  (wave 0; other waves per column); in-kernel clock GHz per wave: " + " ".join(f"{c:.3f}" for c in clk))
 for k, nm in enumerate(names):
     if not nm: continue
