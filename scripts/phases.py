@@ -37,6 +37,19 @@ PHASES = {
 MOVE_SLOTS = [83, 84, 85, 86, 87]
 
 
+def _decile(f, game, sp):
+    order = np.argsort(game)
+    n = max(len(game) // 10, 1)
+    slow, mid = order[-n:], order[len(game) // 2 - n // 2:len(game) // 2 - n // 2 + n]
+    lens = np.array([sp.engine.record(int(g))["length"] for g in range(len(game))])
+
+    def per(idx):
+        return {k: float(f[idx][:, v].sum(1).mean()) for k, v in PHASES.items()}
+    return {"games": int(n), "cycles_slowest": per(slow), "cycles_median_decile": per(mid),
+            "moves_slowest": float(lens[slow].mean()), "moves_median_decile": float(lens[mid].mean()),
+            "moves_all": float(lens.mean())}
+
+
 def main():
     import mzgo
     from mzgo import _lib
@@ -94,6 +107,9 @@ def main():
             "jobs_served": float(f[:, 46].sum()), "tail_phase_cycles_per_game": float(f[:, 47].mean()),
             "idle_cu_share_with_helpers": float(1 - (game.sum() + f[:, 44].sum()) / (len(game) * game.max())),
         },
+        # what the slowest games (the epoch's tail) spend their cycles on,
+        # against the median decile, and how long their games are
+        "slowest_decile": _decile(f, game, sp),
         # every slot's mean per game (lap slots: thread 0's partition; others:
         # wave sums / counters, mzgo_common.hpp's map)
         "slots_mean_per_game": {int(i): round(float(f[:, i].mean())) for i in range(f.shape[1]) if f[:, i].any()},
