@@ -123,6 +123,13 @@ struct TowerHost {
     for (const ChainBuf& c : chains)
       if (c.host.size() == L.size() && std::memcmp(c.host.data(), L.data(), L.size() * sizeof(TConvArgs)) == 0)
         dev = c.dev;
+    if (!dev && chains.size() >= 16) {
+      // (inference calls on changing scratch buffers: keep the table cache
+      // bounded; stream-ordered, so wait for launches still reading them)
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+      for (ChainBuf& c : chains) (void)hipFree(c.dev);
+      chains.clear();
+    }
     if (!dev) {
       ChainBuf c;
       c.host = L;
