@@ -158,6 +158,12 @@ def phases_summary(workload, moves_per_launch):
         out["tail_idle_cu_share_with_helpers"] = round(th["idle_cu_share_with_helpers"], 4)
         out["tail_convs_share"] = round(p["engine_counters"]["tail_convs"] /
                                         max(1, p["engine_counters"]["dynamics_convs"]), 4)
+    sd = p.get("slowest_decile")
+    if sd:
+        # the epoch's slowest games against the median decile, per phase (the tail's make-up)
+        out["slowest_decile_vs_median"] = {k: round(v / max(sd["cycles_median_decile"][k], 1.0), 3)
+                                           for k, v in sd["cycles_slowest"].items()}
+        out["moves_per_game"] = {"slowest_decile": sd["moves_slowest"], "all": sd["moves_all"]}
     return out
 
 
