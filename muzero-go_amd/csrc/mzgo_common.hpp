@@ -166,6 +166,30 @@ __device__ __forceinline__ int tid_local() {
   return t;
 }
 
+// a / b in f64, correctly rounded, for the search's divisions (q = W / N,
+// (q - lo) / (hi - lo), c P sqrt(N) / (1 + n)): the reciprocal, two Newton
+// steps, the product and one FMA correction -- the compiler's sequence for
+// `/` without v_div_scale / v_div_fmas' scaling and v_div_fixup, which only
+// pass values through when a, b and a / b are normal and far from overflow,
+// as these always are (finite value sums, counts >= 1, a positive spread).
+// Bit-identical to `/` there (tools/ddiv_probe.hip: 16.8 M search-like and
+// wide-exponent pairs, no mismatch), 22 against 75 cycles per division; the
+// sign of a zero quotient may differ, which no score, minimum or maximum
+// sees.  MZGO_IEEE_DIV=1 builds plain `/` (A/B).
+__device__ __forceinline__ double ddiv(double a, double b) {
+#ifdef MZGO_IEEE_DIV
+  return a / b;
+#else
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = a * r;
+  return __builtin_fma(__builtin_fma(-b, q, a), r, q);
+#endif
+}
+
 // Order LDS traffic between lanes of one wave (no workgroup barrier needed).
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -1238,7 +1238,7 @@ __device__ __forceinline__ void verify_load_level(Smem<G>& sm, const SearchParam
     }
     const bool e = P > 0.0;
     const uint64_t el = __ballot(e);
-    const double q = e ? (n > 0 ? w / (double)n : 0.0) : 0.0;
+    const double q = e ? (n > 0 ? ddiv(w, (double)n) : 0.0) : 0.0;
     const double cp = l == 0 ? sp.c_puct * P : (double)((float)sp.c_puct * (float)P);
     vl.cP[k][a] = cp;
     vl.q[k][a] = q;
@@ -1311,10 +1311,10 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
       bool bad = false;
       if (i <= B) {
         const int n1 = nx + i, Ni = N0 + i;
-        const double qxi = n1 > 0 ? vl.wpre[k][i] / (double)n1 : 0.0;
+        const double qxi = n1 > 0 ? ddiv(vl.wpre[k][i], (double)n1) : 0.0;
         const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
         const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
-        const double sxi = (hii > loi ? (qxi - loi) / (hii - loi) : qxi) + (cpx * sqi) / (double)(1 + n1);
+        const double sxi = (hii > loi ? ddiv(qxi - loi, hii - loi) : qxi) + ddiv(cpx * sqi, (double)(1 + n1));
         vl.qx[k][i] = qxi;
         vl.invr[k][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;
         vl.sq[k][i] = sqi;
@@ -1418,8 +1418,8 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
           const bool isx = a == xa;
           const double q = isx ? qx : vl.q[k][a];
           const int n = isx ? nx : vl.n[k][a];
-          const double qn = hi > lo ? (q - lo) / (hi - lo) : q;
-          const double sc = qn + (vl.cP[k][a] * sq) / (double)(1 + n);
+          const double qn = hi > lo ? ddiv(q - lo, hi - lo) : q;
+          const double sc = qn + ddiv(vl.cP[k][a] * sq, (double)(1 + n));
           beat |= __ballot(el && !isx && (sc > sx || (sc == sx && a < xa)));
         }
         if (beat && lane == 0)

@@ -745,7 +745,7 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
   for (int j = 0; j < G::AP; ++j) {
     q[j] = 0.0;
     if ((elig[j] >> lane) & 1ull) {
-      q[j] = n[j] > 0 ? w[j] / (double)n[j] : 0.0;
+      q[j] = n[j] > 0 ? ddiv(w[j], (double)n[j]) : 0.0;
       lo = fmin(lo, q[j]);
       hi = fmax(hi, q[j]);
     }
@@ -760,10 +760,10 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
   for (int j = 0; j < G::AP; ++j) {
     sc[j] = -INFINITY;
     if ((elig[j] >> lane) & 1ull) {
-      const double qn = hi > lo ? (q[j] - lo) / (hi - lo) : q[j];
+      const double qn = hi > lo ? ddiv(q[j] - lo, hi - lo) : q[j];
       double u;
-      if (root) u = ((sp.c_puct * P[j]) * sq) / (double)(1 + n[j]);
-      else u = ((double)((float)sp.c_puct * (float)P[j]) * sq) / (double)(1 + n[j]);
+      if (root) u = ddiv((sp.c_puct * P[j]) * sq, (double)(1 + n[j]));
+      else u = ddiv((double)((float)sp.c_puct * (float)P[j]) * sq, (double)(1 + n[j]));
       sc[j] = qn + u;
     }
   }
