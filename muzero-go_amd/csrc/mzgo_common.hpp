@@ -229,10 +229,29 @@ __device__ __forceinline__ double lane(double v, int l) {
 // against the DPP + readlane version with compare-and-select.)  The values
 // reduced here are finite; a -0 / +0 tie may come out with either sign,
 // which changes no score the search forms from it.
-__device__ __forceinline__ float fmin_(float a, float b) { return fminf(a, b); }
-__device__ __forceinline__ float fmax_(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ double fmin_(double a, double b) { return fmin(a, b); }
-__device__ __forceinline__ double fmax_(double a, double b) { return fmax(a, b); }
+// (v_min / v_max directly: fmin / fmax lower to llvm.minnum, which in IEEE
+// mode quiets signalling NaNs with a v_max x, x, x on each operand first --
+// two extra f64 operations per reduction step for values that are finite)
+__device__ __forceinline__ float fmin_(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float fmax_(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double fmin_(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double fmax_(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 template <bool S32>
 __device__ __forceinline__ void lane_swap(unsigned x, unsigned& a, unsigned& b) {
   const auto r = S32 ? __builtin_amdgcn_permlane32_swap(x, x, false, false)
