@@ -1245,7 +1245,7 @@ __device__ __forceinline__ void verify_load_level(Smem<G>& sm, const SearchParam
     vl.inv1n[k][a] = 1.0 / (double)(1 + n);
     vl.n[k][a] = n;
     if (lane == 0) vl.elig[k][j] = el;
-    if (e && a != xa) { lo = fmin(lo, q); hi = fmax(hi, q); }
+    if (e && a != xa) { lo = fmin_(lo, q); hi = fmax_(hi, q); }
     if (j == (xa >> 6)) {
       nx = __builtin_amdgcn_readlane(n, xa & 63);
       cpx = dpp::lane(cp, xa & 63);
@@ -1312,7 +1312,7 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
       if (i <= B) {
         const int n1 = nx + i, Ni = N0 + i;
         const double qxi = n1 > 0 ? ddiv(vl.wpre[k][i], (double)n1) : 0.0;
-        const double loi = fmin(lo, qxi), hii = fmax(hi, qxi);
+        const double loi = fmin_(lo, qxi), hii = fmax_(hi, qxi);
         const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
         const double sxi = (hii > loi ? ddiv(qxi - loi, hii - loi) : qxi) + ddiv(cpx * sqi, (double)(1 + n1));
         vl.qx[k][i] = qxi;
@@ -1347,8 +1347,8 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
       const int i = lane + 64 * j;
       const int ii = i <= B ? i : B;
       const double qxi = vl.qx[k][ii];
-      loi[j] = fmin(lo_o, qxi);
-      spread[j] = fmax(hi_o, qxi) > loi[j];
+      loi[j] = fmin_(lo_o, qxi);
+      spread[j] = fmax_(hi_o, qxi) > loi[j];
       invr[j] = vl.invr[k][ii];
       sqi[j] = vl.sq[k][ii];
       sxi[j] = vl.sx[k][ii];
@@ -1408,7 +1408,7 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
         const int xa = vl.x[k];
         const int nx = vl.n0[k] + i;
         const double qx = vl.qx[k][i];
-        const double lo = fmin(vl.lo_o[k], qx), hi = fmax(vl.hi_o[k], qx);
+        const double lo = fmin_(vl.lo_o[k], qx), hi = fmax_(vl.hi_o[k], qx);
         const double sq = vl.sq[k][i], sx = vl.sx[k][i];
         uint64_t beat = 0;
 #pragma unroll

@@ -172,7 +172,7 @@ __device__ __forceinline__ void softmax_regs(const float (&x)[G::AP], float (&p)
   float m = -INFINITY;
 #pragma unroll
   for (int j = 0; j < G::AP; ++j)
-    if (lane + 64 * j < G::A) m = fmaxf(m, x[j]);
+    if (lane + 64 * j < G::A) m = fmax_(m, x[j]);
   m = wave_max(m);
   float s = 0.f;
 #pragma unroll
@@ -746,8 +746,8 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
     q[j] = 0.0;
     if ((elig[j] >> lane) & 1ull) {
       q[j] = n[j] > 0 ? ddiv(w[j], (double)n[j]) : 0.0;
-      lo = fmin(lo, q[j]);
-      hi = fmax(hi, q[j]);
+      lo = fmin_(lo, q[j]);
+      hi = fmax_(hi, q[j]);
     }
   }
   if (st) st->lap(25);
