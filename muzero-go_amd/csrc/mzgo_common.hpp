@@ -190,6 +190,27 @@ __device__ __forceinline__ double ddiv(double a, double b) {
 #endif
 }
 
+// sqrt in f64, correctly rounded, of the search's visit counts (integers
+// >= 1): the reciprocal square root and the compiler's Newton / correction
+// steps without the scaling of tiny arguments and the zero / infinity / NaN
+// selects.  Bit-identical to sqrt for every integer 1 .. 2^24 and 16.8 M
+// wide-exponent arguments (tools/ddiv_probe.hip).  MZGO_IEEE_DIV=1: sqrt.
+__device__ __forceinline__ double dsqrt(double x) {
+#ifdef MZGO_IEEE_DIV
+  return sqrt(x);
+#else
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+#endif
+}
+
 // Order LDS traffic between lanes of one wave (no workgroup barrier needed).
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -1313,7 +1313,7 @@ __device__ __forceinline__ void verify_levels(Smem<G>& sm, const SearchParams& s
         const int n1 = nx + i, Ni = N0 + i;
         const double qxi = n1 > 0 ? ddiv(vl.wpre[k][i], (double)n1) : 0.0;
         const double loi = fmin_(lo, qxi), hii = fmax_(hi, qxi);
-        const double sqi = sp.variant == 1 ? sqrt((double)(Ni + 1)) : sqrt((double)(Ni > 1 ? Ni : 1));
+        const double sqi = dsqrt((double)(sp.variant == 1 ? Ni + 1 : (Ni > 1 ? Ni : 1)));
         const double sxi = (hii > loi ? ddiv(qxi - loi, hii - loi) : qxi) + ddiv(cpx * sqi, (double)(1 + n1));
         vl.qx[k][i] = qxi;
         vl.invr[k][i] = hii > loi ? 1.0 / (hii - loi) : 0.0;

@@ -754,7 +754,7 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
   wave_minmax(lo, hi);
   if (st) st->lap(26);
   // sqrt(max(1, N)) (self_play.py:316) or sqrt(N + 1) (main.py:354)
-  const double sq = sp.variant == 1 ? sqrt((double)(nvis + 1)) : sqrt((double)(nvis > 1 ? nvis : 1));
+  const double sq = dsqrt((double)(sp.variant == 1 ? nvis + 1 : (nvis > 1 ? nvis : 1)));
   double sc[G::AP];
 #pragma unroll
   for (int j = 0; j < G::AP; ++j) {

@@ -1,4 +1,5 @@
-// ddiv_probe.hip -- f64 division without v_div_scale / v_div_fixup (the
+// ddiv_probe.hip -- f64 division without v_div_scale / v_div_fixup, and f64
+// square root without its scaling / class steps (the
 // operands of the search's divisions are normal and their quotients far from
 // overflow / underflow, where those two only pass values through): bit
 // equality with a / b over random search-like operands, and cycles per
@@ -21,11 +22,27 @@ __device__ __forceinline__ double ddiv_fast(double a, double b) {
   return __builtin_fma(res, r, q);
 }
 
+__device__ __forceinline__ double dsqrt_fast(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+
 __global__ void k_check(const double* a, const double* b, unsigned long long* bad, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double x = a[i] / b[i], y = ddiv_fast(a[i], b[i]);
   if (__double_as_longlong(x) != __double_as_longlong(y)) atomicAdd(bad, 1ull);
+  // square roots: the integers 1 .. n and |a| (wide exponents)
+  const double s1 = (double)(i + 1), s2 = fabs(a[i]) + 1e-300;
+  if (__double_as_longlong(sqrt(s1)) != __double_as_longlong(dsqrt_fast(s1))) atomicAdd(bad + 1, 1ull);
+  if (__double_as_longlong(sqrt(s2)) != __double_as_longlong(dsqrt_fast(s2))) atomicAdd(bad + 1, 1ull);
 }
 
 template <int FAST>
@@ -57,19 +74,19 @@ int main() {
   }
   double *da, *db, *sink;
   unsigned long long *dbad, *dcyc;
-  hipMalloc(&da, n * 8); hipMalloc(&db, n * 8); hipMalloc(&dbad, 8); hipMalloc(&dcyc, 16); hipMalloc(&sink, 64 * 8);
+  hipMalloc(&da, n * 8); hipMalloc(&db, n * 8); hipMalloc(&dbad, 16); hipMalloc(&dcyc, 16); hipMalloc(&sink, 64 * 8);
   hipMemcpy(da, a.data(), n * 8, hipMemcpyHostToDevice);
   hipMemcpy(db, b.data(), n * 8, hipMemcpyHostToDevice);
-  hipMemset(dbad, 0, 8);
+  hipMemset(dbad, 0, 16);
   hipLaunchKernelGGL(k_check, dim3(n / 256), dim3(256), 0, 0, da, db, dbad, n);
   hipLaunchKernelGGL(k_time<0>, dim3(1), dim3(64), 0, 0, da, db, dcyc, sink);
   hipLaunchKernelGGL(k_time<1>, dim3(1), dim3(64), 0, 0, da, db, dcyc, sink);
   hipLaunchKernelGGL(k_time<0>, dim3(1), dim3(64), 0, 0, da, db, dcyc, sink);
   hipLaunchKernelGGL(k_time<1>, dim3(1), dim3(64), 0, 0, da, db, dcyc, sink);
-  unsigned long long bad = 0, cyc[2];
-  hipMemcpy(&bad, dbad, 8, hipMemcpyDeviceToHost);
+  unsigned long long bad[2] = {0, 0}, cyc[2];
+  hipMemcpy(bad, dbad, 16, hipMemcpyDeviceToHost);
   hipMemcpy(cyc, dcyc, 16, hipMemcpyDeviceToHost);
-  printf("{\"pairs\": %d, \"mismatches\": %llu, \"cycles_per_div_ieee\": %.1f, \"cycles_per_div_fast\": %.1f}\n", n, bad,
+  printf("{\"pairs\": %d, \"mismatches\": %llu, \"sqrt_mismatches\": %llu, \"cycles_per_div_ieee\": %.1f, \"cycles_per_div_fast\": %.1f}\n", n, bad[0], bad[1],
          cyc[0] / 4096.0, cyc[1] / 4096.0);
   return 0;
 }
