@@ -545,7 +545,10 @@ struct TConvKsGeo {
 #ifdef MZGO_TCONV_KS_ADIST
   static constexpr int ADIST = MZGO_TCONV_KS_ADIST;
 #else
-  static constexpr int ADIST = 2;      // 1 and 3 spill at N = 19
+  // 1 since round 4: 0 B scratch in k_tconv_ks and k_tconv_chain (2 left the
+  // chain kernel 40 B of spills), config 5 1535-1537 -> 1514-1516 ms per move
+  // (same call); 3 spills
+  static constexpr int ADIST = 1;
 #endif
   static_assert(ADIST >= 1 && ADIST <= 3 * MT, "A prefetch distance");
   static_assert(8 * MT * 2 * 1024 <= 2 * T::PB + 2 * T::WSLOT, "the epilogue's accumulator exchange fits the patch buffers + ring");
