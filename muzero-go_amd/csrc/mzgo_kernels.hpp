@@ -1203,6 +1203,15 @@ __device__ __forceinline__ bool replay_sequential(int B, int depth) {
   if constexpr (MZGO_VERIFY_SEQ_K > 0) return (B - 1) * (depth + 1) < MZGO_VERIFY_SEQ_K;
   else return B < kVerifyMinB;
 }
+// HBM trees with helper workgroups (shared jobs): the same rule with its own K
+// (0: always the shared parallel replay)
+#ifndef MZGO_SHARED_SEQ_K
+#define MZGO_SHARED_SEQ_K 0
+#endif
+__device__ __forceinline__ bool replay_parallel(bool shared, int B, int depth) {
+  if (shared) return !(MZGO_SHARED_SEQ_K > 0 && (B - 1) * (depth + 1) < MZGO_SHARED_SEQ_K);
+  return !replay_sequential(B, depth);
+}
 
 // Phase 1a of verify_batch for one path level l (row k of vl): its
 // children's c_puct * P, q, 1 / (1 + n), n and eligibility, the min / max of
@@ -1887,7 +1896,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         if (shared_jobs<G>(sp)) {
           batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf, um, nun - 1, 1, key,
                                            sim + 1, &st, prepicked, [&]() {
-                                             if (depth <= kVerifyMaxDepth) verify_preload<G, Acc>(sm, sp, TV, T, nact, depth);
+                                             if (depth <= kVerifyMaxDepth && replay_parallel(true, B, depth))
+                                               verify_preload<G, Acc>(sm, sp, TV, T, nact, depth);
                                            });
           st.lap(71);
         } else {
@@ -1906,7 +1916,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         }
         __syncthreads();
         st.lap(5);
-        if (depth <= kVerifyMaxDepth && (shared_jobs<G>(sp) || !replay_sequential(B, depth))) {
+        if (depth <= kVerifyMaxDepth && replay_parallel(shared_jobs<G>(sp), B, depth)) {
           const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st, shared_jobs<G>(sp));
           nodes += m;
           sim += m;
