@@ -1204,9 +1204,9 @@ __device__ __forceinline__ bool replay_sequential(int B, int depth) {
   else return B < kVerifyMinB;
 }
 // HBM trees with helper workgroups (shared jobs): the same rule with its own K
-// (0: always the shared parallel replay)
+// (0: always the shared parallel replay; 32: profiles/r4x_shared_seq_ab.txt)
 #ifndef MZGO_SHARED_SEQ_K
-#define MZGO_SHARED_SEQ_K 0
+#define MZGO_SHARED_SEQ_K 32
 #endif
 __device__ __forceinline__ bool replay_parallel(bool shared, int B, int depth) {
   if (shared) return !(MZGO_SHARED_SEQ_K > 0 && (B - 1) * (depth + 1) < MZGO_SHARED_SEQ_K);
