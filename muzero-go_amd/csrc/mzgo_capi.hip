@@ -573,8 +573,21 @@ int mzgo_recurrent_inference(mzgo_engine* e, const float* latent, const int64_t*
   return MZGO_OK;
 }
 
+// Tower engines: a k_tconv_chain wait that expired makes that launch's
+// results wrong; it is reported (MZGO_EHIP) and cleared by the first API
+// call that synchronises afterwards -- every call of the tower path does
+// (self-play moves, search, inference checks, tree / record / counter reads).
+static int check_chain(mzgo_engine* e, hipStream_t s) {
+  if (!e->tower) return MZGO_OK;
+  bool bad = false;
+  HIPCHK(e->tower->chain_error(s, bad));
+  if (bad) return fail(MZGO_EHIP, "k_tconv_chain: a workgroup's wait for its board expired (results of the call are wrong)");
+  return MZGO_OK;
+}
+
 int mzgo_check_inference_errors(mzgo_engine* e, void* stream) {
   if (!e) return fail(MZGO_EINVAL, "null engine");
+  if (int rc = check_chain(e, (hipStream_t)stream)) return rc;
   int h = 0;
   HIPCHK(hipMemcpyAsync(&h, e->d_err, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
@@ -599,7 +612,7 @@ int mzgo_search(mzgo_engine* e, const float* root_obs, const double* noise, int 
     HIPCHK(t.root_phase(sp, e->E, noise, e->A, 0, s));
     HIPCHK(t.simulations(sp, e->E, s));
     HIPCHK(t.ts->search_out(t.TA, sp, e->E, G, visits, value, s));
-    return MZGO_OK;
+    return check_chain(e, s);
   }
   HIPCHK(e->ks->search(e->np, e->search_params(), e->E, root_obs, noise, G, e->cfg.game_base, move_index,
                        visits, value, (hipStream_t)stream));
@@ -617,6 +630,7 @@ int mzgo_tree_export(mzgo_engine* e, int g, int32_t* n_nodes, int32_t* child, in
     // API does (k_tsearch_out; idempotent, the values a later select would form)
     TowerHost& t = *e->tower;
     HIPCHK(t.ts->search_out(t.TA, e->search_params(), e->E, e->G, nullptr, nullptr, s));
+    if (int rc = check_chain(e, s)) return rc;
   }
   int nn = 0;
   HIPCHK(hipMemcpyAsync(&nn, e->E.nodes + g, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -671,6 +685,32 @@ int mzgo_selfplay_reset(mzgo_engine* e, int epoch, void* stream) {
 // k_selfplay_move; boards whose batch expansions stream Y from L2 (19x19) get
 // helper workgroups, 3 per game by default (MZGO_HELPERS_PER_GAME), with the
 // job slots zeroed before the launch (batch_expand_shared)
+// CUs of the current device (one self-play workgroup fills a CU's LDS)
+static int device_cus() {
+  static int ncu = -1;
+  if (ncu < 0) {
+    int dev = 0;
+    ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 0;
+  }
+  return ncu;
+}
+
+// The epoch tail (whole-game launches): a workgroup whose game has ended
+// stays resident and serves running games.  Only when every workgroup of the
+// launch is resident at once (one per CU): otherwise ended workgroups would
+// hold CUs that games not yet dispatched are waiting for.  MZGO_TAIL_HELPERS=0
+// turns it off, =2 forces it on past that bound (a test of the kernel's own
+// guards: helpers never join a game whose workgroup has not started).
+static bool tail_enabled(int workgroups) {
+  const char* v = getenv("MZGO_TAIL_HELPERS");
+  const int mode = v ? atoi(v) : 1;
+  if (mode == 0) return false;
+  return mode == 2 || workgroups <= device_cus();
+}
+
 static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayParams& pp, hipStream_t s) {
   SearchParams sp = e->search_params();
   if (e->ks->shared_batches) {
@@ -678,19 +718,13 @@ static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayPara
     if (const char* v = getenv("MZGO_HELPERS_PER_GAME")) per = atoi(v);
     sp.helpers = per > 0 ? per * e->G : 0;
     HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
-    // the epoch tail: helpers (and workgroups) of ended games join running
-    // games (whole-game launches; MZGO_TAIL_HELPERS=0 turns it off)
-    const char* v = getenv("MZGO_TAIL_HELPERS");
-    if (sp.helpers > 0 && sp.factored && pp.moves > 1 && !(v && atoi(v) == 0)) sp.tail = 1;
-  } else if (e->ks->tail_convs && sp.factored && pp.moves > 1) {
-    // the epoch tail (one-strip Winograd boards, whole games per launch): a
-    // workgroup whose game has ended serves running games' parent convs
-    // (MZGO_TAIL_HELPERS=0 turns it off; the records are the same either way)
-    const char* v = getenv("MZGO_TAIL_HELPERS");
-    if (!(v && atoi(v) == 0)) {
-      sp.tail = 1;
-      HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
-    }
+    // the epoch tail: helpers (and workgroups) of ended games join running games
+    if (sp.helpers > 0 && sp.factored && pp.moves > 1 && tail_enabled(e->G + sp.helpers)) sp.tail = 1;
+  } else if (e->ks->tail_convs && sp.factored && pp.moves > 1 && tail_enabled(e->G)) {
+    // the epoch tail (one-strip Winograd boards): a workgroup whose game has
+    // ended serves running games' parent convs (records the same either way)
+    sp.tail = 1;
+    HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)e->G * job_bytes(e->A), s));
   }
   HIPCHK(e->ks->selfplay_move(e->np, np_b, sp, pp, e->E, e->G, s));
   return MZGO_OK;
@@ -725,9 +759,7 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
       if (k > 0 && k % 4 == 0) {
         HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        bool bad = false;
-        HIPCHK(t.chain_error(s, bad));
-        if (bad) return fail(MZGO_EHIP, "k_tconv_chain: a workgroup's wait for its board expired");
+        if (int rc = check_chain(e, s)) return rc;
         bool any = false;
         for (int v : st) any |= v == 0;
         if (!any) break;
@@ -737,7 +769,9 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
       HIPCHK(t.simulations(sp, e->E, s));
       HIPCHK(t.ts->choose(t.TA, sp, pp, e->E, e->G, s));
     }
-    return MZGO_OK;
+    // (a tower move is ~1.5 s of device work: one synchronisation per call
+    // reports an expired chain wait of this call, MZGO_EHIP, and clears it)
+    return check_chain(e, s);
   }
   return launch_selfplay(e, e->np, pp, (hipStream_t)stream);
 }
@@ -845,6 +879,7 @@ int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   HIPCHK(hipMemcpyAsync(c, e->E.counters, sizeof c, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (int rc = check_chain(e, s)) return rc;
   int playing = 0;
   for (int v : st) playing += v == 0;
   out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing; out[4] = c[3]; out[5] = c[4];
@@ -860,6 +895,7 @@ int mzgo_records_export(mzgo_engine* e, int g, int32_t* length, int32_t* status,
   HIPCHK(hipMemcpyAsync(meta, e->E.meta + (size_t)g * 4, 16, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&st, e->E.status + g, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (int rc = check_chain(e, s)) return rc;
   const int L = meta[3];
   if (length) *length = L;
   if (status) *status = st;

@@ -241,6 +241,8 @@ struct ExpandPlan {
 // same address), so no lane is masked off; the last pass's cells past the
 // board land in the row padding and stay out of S.  Wave-level; the caller
 // orders xw for the wave's readers (wave_lds_sync).
+// POL = false (lazy policy head, batched children): the totals only; the
+// policy sums are formed if a select ever reaches the child (policy_sums_wg).
 // GLOBAL_Y boards: Y loads one pass pair ahead (MZGO_NO_EXPAND_PREFETCH for
 // the A/B build without; the same values either way)
 #ifdef MZGO_NO_EXPAND_PREFETCH
@@ -248,7 +250,7 @@ constexpr bool kExpandPrefetch = false;
 #else
 constexpr bool kExpandPrefetch = true;
 #endif
-template <class G, int PROW>
+template <class G, int PROW, bool POL = true>
 __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw,
                                             const ExpandPlan<G>& plan, float& rsum, float& vsum) {
   typedef ExpandShape<G> X;
@@ -260,7 +262,7 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   f32x2 s2[X::PERL][2];
 #pragma unroll
   for (int k = 0; k < X::PERL; ++k) {
-    wp[k] = W4[2 * X::C4 + j + 8 * k];
+    if constexpr (POL) wp[k] = W4[2 * X::C4 + j + 8 * k];
     s2[k][0] = f32x2{0.f, 0.f};
     s2[k][1] = f32x2{0.f, 0.f};
   }
@@ -285,12 +287,12 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
         f32x2 v = f32x2{y[k][q], y[k][q + 1]} + f32x2{e[k][q], e[k][q + 1]};
         v.x = v.x > 0.f ? v.x : 0.f;
         v.y = v.y > 0.f ? v.y : 0.f;
-        hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
+        if constexpr (POL) hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
         if (!live) v = f32x2{0.f, 0.f};
         s2[k][q >> 1] = s2[k][q >> 1] + v;
       }
     }
-    xr[8 * p] = sum8(hp2.x + hp2.y);
+    if constexpr (POL) xr[8 * p] = sum8(hp2.x + hp2.y);
   };
   (void)pass_y;
   auto pass = [&](int p, uint32_t eoff, bool last) {
@@ -314,12 +316,12 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
         f32x2 v = f32x2{y[k][q], y[k][q + 1]} + f32x2{e[k][q], e[k][q + 1]};
         v.x = v.x > 0.f ? v.x : 0.f;
         v.y = v.y > 0.f ? v.y : 0.f;
-        hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
+        if constexpr (POL) hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
         if (!live) v = f32x2{0.f, 0.f};
         s2[k][q >> 1] = s2[k][q >> 1] + v;
       }
     }
-    xr[8 * p] = sum8(hp2.x + hp2.y);
+    if constexpr (POL) xr[8 * p] = sum8(hp2.x + hp2.y);
   };
   if constexpr (ExpandPlan<G>::TABLE) {
     // every pass unrolled, offsets from the plan's registers
@@ -370,6 +372,87 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   }
   rsum = wave_sum(dr2.x + dr2.y);
   vsum = wave_sum(dv2.x + dv2.y);
+}
+
+// Lazy policy head.  A batched child's policy logits are read only when a
+// select first reaches it (~3 % of children: the reference's trees are wide),
+// so batch expansions skip the policy 1x1 conv (expand_wave<..., false>) and
+// the logits of such a node are formed on its first arrival from its parent's
+// Y and its E[a] -- the child latent relu(Y + E[a]) rebuilt -- with
+// expand_wave's operations in its order per cell (8 lanes per cell, lane j
+// channels c4 = j + 8k, packed FMAs, the 3-step DPP sum): bit-identical to
+// the sums the eager expansion wrote (self_play.py:104-112 on the child's
+// latent, :204-207).
+//
+// One cell's policy sum (no bias) by the 8 lanes of a lane group.
+template <class G>
+__device__ __forceinline__ float policy_cell(const float* __restrict__ Y, const float* __restrict__ ea,
+                                             const f32x4 (&wp)[ExpandShape<G>::PERL], int cell, int j) {
+  typedef ExpandShape<G> X;
+  const int cl = cell < G::CELLS ? cell : G::CELLS - 1;
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(Y) + (size_t)cl * X::C4 + j;
+  const f32x4* E4 = reinterpret_cast<const f32x4*>(ea) + region_of<G>(cl) * X::C4 + j;
+  f32x4 y[X::PERL], e[X::PERL];
+#pragma unroll
+  for (int k = 0; k < X::PERL; ++k) {
+    y[k] = Y4[8 * k];
+    e[k] = E4[8 * k];
+  }
+  f32x2 hp2 = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < X::PERL; ++k) {
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      f32x2 v = f32x2{y[k][q], y[k][q + 1]} + f32x2{e[k][q], e[k][q + 1]};
+      v.x = v.x > 0.f ? v.x : 0.f;
+      v.y = v.y > 0.f ? v.y : 0.f;
+      hp2 = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, v, hp2);
+    }
+  }
+  return sum8(hp2.x + hp2.y);
+}
+
+template <class G>
+__device__ __forceinline__ void policy_weights(const float* hw, f32x4 (&wp)[ExpandShape<G>::PERL], int j) {
+  typedef ExpandShape<G> X;
+  const f32x4* W4 = reinterpret_cast<const f32x4*>(hw);
+#pragma unroll
+  for (int k = 0; k < X::PERL; ++k) wp[k] = W4[2 * X::C4 + j + 8 * k];
+}
+
+// The policy sums of every cell of one node -> out[CELLS] (LDS), by the whole
+// workgroup: lane group (wave, cg) takes cells 8 wave + cg + 8 WAVES r.  Y: the
+// parent's [CELLS][C] (HBM), ea: E[a] [9][C], hw: head weights [3][C].  All
+// threads; the caller synchronises before reading out.
+template <class G>
+__device__ __forceinline__ void policy_sums_wg(float* out, const float* __restrict__ Y, const float* __restrict__ ea,
+                                               const float* hw) {
+  const int lane = lane_id_local(), j = lane & 7;
+  const int slot = 8 * (tid_local() >> 6) + (lane >> 3);
+  constexpr int SLOTS = 8 * G::WAVES, R = (G::CELLS + SLOTS - 1) / SLOTS;
+  f32x4 wp[ExpandShape<G>::PERL];
+  policy_weights<G>(hw, wp, j);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int cell = slot + SLOTS * r;
+    const float s = policy_cell<G>(Y, ea, wp, cell, j);
+    if (cell < G::CELLS) out[cell] = s;
+  }
+}
+
+// The same by one wave (lane group cg: cells cg + 8 p) -> out[CELLS] (LDS).
+// The caller orders out for the wave's readers (wave_lds_sync).
+template <class G>
+__device__ __forceinline__ void policy_sums_wave(float* out, const float* __restrict__ Y,
+                                                 const float* __restrict__ ea, const float* hw) {
+  const int lane = lane_id_local(), j = lane & 7, cg = lane >> 3;
+  f32x4 wp[ExpandShape<G>::PERL];
+  policy_weights<G>(hw, wp, j);
+  for (int p = 0; p < (G::CELLS + 7) / 8; ++p) {
+    const int cell = cg + 8 * p;
+    const float s = policy_cell<G>(Y, ea, wp, cell, j);
+    if (cell < G::CELLS) out[cell] = s;
+  }
 }
 
 // The latent of a node that is about to become a parent: relu(Y_par + E[a])

@@ -379,8 +379,8 @@ __device__ __forceinline__ float* pool_of(const EngineArrays& E, int g) {
 // Batch expansion (factored dynamics): children i < B of one parent whose Y
 // is in L.yc (and the head weights in L.hw), child i = node nid0 + i via
 // action L.acts[i]; one wave per child: E[a] into LDS, heads, the child's
-// prior row (LAZY: its logits, see TreeLds::rawp) and child row, L.bv[i] =
-// its backup value r + discount * v.  Each wave claims the next child
+// prior row and child row (LAZY: neither -- the lazy policy head, see
+// TreeLds::rawp), L.bv[i] = its backup value r + discount * v.  Each wave claims the next child
 // (sm.t.ngrab, reset with sm.t.npick by the caller) and waits until
 // sm.t.npick > k (wave 0 publishes the actions, pick_sequence, before it
 // joins).  All threads; the caller synchronises.
@@ -425,8 +425,8 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
       wave_lds_sync();
       if (st) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
       float rsum, vsum;
-      if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
-      else expand_wave<G, XL::PROW>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
+      if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW, !LAZY>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+      else expand_wave<G, XL::PROW, !LAZY>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
       wave_lds_sync();
       epre_a = -1;
       kn = grab();
@@ -439,23 +439,18 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
         }
       }
       if (st) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
-      float r, v, x[G::AP];
+      float r, v;
       heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
-      policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
-      if constexpr (!LAZY) {                 // (a lazy child's row is written when it is settled)
-        int* crow = TV.child + (size_t)nid * G::A;
-        for (int i = lane; i < G::A; i += 64) crow[i] = -1;
-      }
       if (st) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
       if constexpr (LAZY) {
-        // the row keeps the logits until a select first reaches the child
-        // (select_leaf -> settle_priors); most children never are
-        float* prow = TV.prior + (size_t)nid * G::A;
-#pragma unroll
-        for (int j = 0; j < G::AP; ++j)
-          if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
+        // no policy head: a select that first reaches the child forms its
+        // logits (select_leaf -> kNeedLogits -> policy_sums_wg); most never do
         if (lane == 0) atomicOr(&sm.t.rawp[nid >> 5], 1u << (nid & 31));
       } else {
+        float x[G::AP];
+        policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
+        int* crow = TV.child + (size_t)nid * G::A;
+        for (int i = lane; i < G::A; i += 64) crow[i] = -1;
         child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
       }
       if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
@@ -515,6 +510,10 @@ struct JobView {
   __device__ double* pass_prior() const { return reinterpret_cast<double*>(base + 224); }
   // replay checks: the failing simulations found by every workgroup (bit i)
   __device__ unsigned long long* failm() const { return reinterpret_cast<unsigned long long*>(base + 256); }
+  // 1 once the game's workgroup runs (zeroed by the host before the launch):
+  // tail helpers join only started games -- one not yet dispatched may be
+  // waiting for the very CU a helper holds
+  __device__ unsigned* started() const { return reinterpret_cast<unsigned*>(base + 384); }
   // tail helpers registered with this game (9x9 whole-game launches, tail_help)
   __device__ unsigned* nhelp() const { return reinterpret_cast<unsigned*>(base + 448); }
   // the actions, tagged: batch number << 32 | action (an entry is valid for
@@ -759,7 +758,9 @@ __device__ __forceinline__ void tail_help(Smem<G>& sm, const NetParams& np_a, co
         for (int k = 1; k < games && pick < 0; ++k) {
           const int t = (self + k) % games;
           const JobView Jt = job_of<G>(E, t);
-          if (__hip_atomic_load(Jt.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kJobExit) continue;
+          if (__hip_atomic_load(Jt.started(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 ||
+              __hip_atomic_load(Jt.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kJobExit)
+            continue;
           unsigned c = __hip_atomic_load(Jt.nhelp(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           while (c < kTailHelpers &&
                  !__hip_atomic_compare_exchange_strong(Jt.nhelp(), &c, c + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -783,17 +784,22 @@ __device__ __forceinline__ void tail_help(Smem<G>& sm, const NetParams& np_a, co
             __builtin_amdgcn_s_sleep(8);
             s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
-          if (s == last || s == 0) {                   // (bounded wait: leave this game)
+          int expired = 0;
+          if (s == last || s == 0) {                   // (bounded wait: leave, and exit -- no re-registering)
             __hip_atomic_fetch_sub(J.nhelp(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s = kJobExit;
+            expired = 1;
           }
           if (s != kJobExit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           sm.bc[2] = (int)s;
+          sm.bc[4] = expired;
         }
         __syncthreads();
         const unsigned s = (unsigned)sm.bc[2];
+        const int expired = sm.bc[4];
         __syncthreads();
+        if (expired) return;
         if (s == kJobExit) break;
         last = s;
         const int* info = J.info();
@@ -870,11 +876,12 @@ __device__ __forceinline__ void rep_shared(Smem<G>& sm, const NetParams& np, con
 }
 
 // One child of a batch by ONE wave (batch_expand's per-child work): E[a]
-// into W.ew, expand_wave over Y, the heads, the child's prior row (LAZY: its
-// logits) and child row; returns the backup value r + discount * v (every lane).
-// LAZYH (HBM trees, the shared batches): the prior row keeps the logits and
-// the child row gets only the sentinel kRawRow in entry 0; select_leaf turns
-// the row into priors when a select first reaches the node (most never are).
+// into W.ew, expand_wave over Y, the heads, the child's prior row and child
+// row; returns the backup value r + discount * v (every lane).  Lazy policy
+// head: LAZY (LDS trees) writes neither row (TreeLds::rawp), LAZYH (HBM
+// trees, the shared batches) only the sentinel kLazyRow into child-row entry
+// 0; a select that first reaches the node forms its logits and priors (most
+// never are).
 template <class G, bool LAZY, bool LAZYH = false>
 __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                                const TreeView& TV, const float* yg, const ExpandPlan<G>& plan,
@@ -892,27 +899,21 @@ __device__ __forceinline__ double expand_child(Smem<G>& sm, const NetParams& np,
   wave_lds_sync();
   if (st && wave_id() == 0) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
   float rsum, vsum;
-  if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
-  else expand_wave<G, XL::PROW>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
+  constexpr bool POL = !LAZY && !LAZYH;
+  if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW, POL>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+  else expand_wave<G, XL::PROW, POL>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
   wave_lds_sync();
   if (st && wave_id() == 0) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
-  float r, v, x[G::AP];
+  float r, v;
   heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
-  policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
   if (st && wave_id() == 0) { t1 = st->now(); st->wave_add(66, t1 - t0); t0 = t1; }
   if constexpr (LAZY) {
-    float* prow = TV.prior + (size_t)nid * G::A;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
     if (lane == 0) atomicOr(&sm.t.rawp[nid >> 5], 1u << (nid & 31));
   } else if constexpr (LAZYH) {
-    float* prow = TV.prior + (size_t)nid * G::A;
-#pragma unroll
-    for (int j = 0; j < G::AP; ++j)
-      if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
-    if (lane == 0) TV.child[(size_t)nid * G::A] = kRawRow;
+    if (lane == 0) TV.child[(size_t)nid * G::A] = kLazyRow;
   } else {
+    float x[G::AP];
+    policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
     int* crow = TV.child + (size_t)nid * G::A;
     for (int i = lane; i < G::A; i += 64) crow[i] = -1;
     child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
@@ -1702,7 +1703,8 @@ __device__ __forceinline__ int join_running_game(Smem<G>& sm, const EngineArrays
       unsigned key = 0xFFFFFFFFu;
       if (k <= games) {
         const JobView Jt = job_of<G>(E, t);
-        if (__hip_atomic_load(Jt.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kJobExit)
+        if (__hip_atomic_load(Jt.started(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 &&
+            __hip_atomic_load(Jt.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kJobExit)
           key = __hip_atomic_load(Jt.nhelp(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       // (helpers, distance) lexicographic: the fewest helpers, then the nearest
@@ -1752,7 +1754,9 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   constexpr bool BATCH = decltype(sm.u.f)::BATCH;
   Acc T(TV, sm.t);
   tree_reset_root<G>(T);
-  if (tid_local() == 0) { sm.t.newest = -1; sm.t.newp_node = -1; sm.t.ycache = -1; sm.t.rowc_node = -1; }
+  if (tid_local() == 0) {
+    sm.t.newest = -1; sm.t.newp_node = -1; sm.t.ycache = -1; sm.t.rowc_node = -1; sm.t.lognode = -1;
+  }
   __syncthreads();
 
   int nodes = 1, convs = 0;
@@ -1776,6 +1780,21 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       __syncthreads();
     }
     pending = false;
+    // the walk reached a lazily expanded node for the first time: its policy
+    // sums from its parent's Y and E[a] by the whole workgroup, then wave 0
+    // resumes the walk there (it settles the node's priors and goes on)
+    while (sm.t.action == kNeedLogits) {
+      const int xn = sm.t.leaf, xd = sm.t.depth;
+      policy_sums_wg<G>(sm.t.logits, pool + (size_t)sm.t.lpar * node_floats,
+                        np.etab + (size_t)sm.t.lact * 9 * G::C, np.head_w);
+      if (tid_local() == 0) sm.t.lognode = xn;
+      __syncthreads();
+      if (wave_id() == 0) {
+        const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st, xn, xd);
+        if (lane_id() == 0) sm.t.action = a;
+      }
+      __syncthreads();
+    }
     st.lap(0);
     const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;
     if (a < 0) {                                         // terminal leaf: backup 0 (:188-191)
@@ -1966,7 +1985,14 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         continue;
       }
       // ---- one expansion ----
-      if (tid_local() == 0) { T.init(nid); sm.t.newest = nid; }
+      // (nid may be the id of a dropped batch child: clear its lazy mark, the
+      // eager priors below are this node's)
+      if (tid_local() == 0) {
+        T.init(nid);
+        sm.t.newest = nid;
+        if constexpr (G::TREE_CAP > 0)
+          if (nid < G::TREE_CAP) sm.t.rawp[nid >> 5] &= ~(1u << (nid & 31));
+      }
       const unsigned long long t_x = st.now();
       expand_heads<G>(sm.u.f, yleaf, yc == leaf, np.etab + (size_t)a * 9 * G::C, np.head_w);
       if (tid_local() == 0) st.wave_add(56, st.now() - t_x);
@@ -2075,20 +2101,49 @@ __device__ __forceinline__ void search_outputs(const EngineArrays& E, int g, int
   }
 }
 
-// Turn every prior row still holding logits into priors (TreeLds::rawp):
-// the search API exports whole trees (mzgo_tree_export), self-play does not
-// and skips this.  All threads; the batch buffers serve as per-wave scratch.
+// Form the priors of every lazily expanded node no select reached
+// (TreeLds::rawp): the search API exports whole trees (mzgo_tree_export),
+// self-play does not and skips this.  Each wave takes parents p = wave,
+// wave + WAVES, ... and every raw child c = child[p][a]: its policy sums
+// from p's Y and E[a] (policy_sums_wave), then settle_lazy.  All threads;
+// the batch buffers serve as per-wave scratch.
 template <class G>
-__device__ __forceinline__ void settle_all_priors(Smem<G>& sm, const TreeView& TV, int nodes, int variant) {
+__device__ __forceinline__ void settle_all_priors(Smem<G>& sm, const NetParams& np, const EngineArrays& E, int g,
+                                                  int nodes, int variant) {
   if constexpr (decltype(sm.u.f)::BATCH && G::TREE_CAP > 0) {
+    const TreeView TV = TreeViewOf<G>::make(E, g);
+    const float* pool = pool_of<G>(E, g);
     const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+    const int lane = lane_id_local();
     auto& W = sm.u.f.wv[wave];
+    static_assert(sizeof(W.xw) >= sizeof(float) * G::CELLS, "a wave's head rows hold one node's policy sums");
     const int lim = nodes < G::TREE_CAP ? nodes : G::TREE_CAP;
-    for (int n = 1 + wave; n < lim; n += G::WAVES) {
-      if (!sm.t.is_raw(n)) continue;
-      float q[G::AP];
-      settle_priors<G>(sm.t, TV.prior + (size_t)n * G::A, TV.child + (size_t)n * G::A, n, variant, W.fb, W.db, q);
+    if (wave == 0 && lane == 0) sm.t.lognode = -1;
+    for (int p = wave; p < lim; p += G::WAVES) {
+      if (sm.t.is_raw(p)) continue;                  // (no children)
+      for (int a0 = 0; a0 < G::A; a0 += 64) {
+        const int a = a0 + lane;
+        const int c = a < G::A ? TV.child[(size_t)p * G::A + a] : -1;
+        for (uint64_t m = __ballot(c > 0 && c < lim && sm.t.is_raw(c)); m; m &= m - 1) {
+          const int l = __builtin_ctzll(m);
+          const int cc = __builtin_amdgcn_readlane(c, l), ca = a0 + l;
+          policy_sums_wave<G>(W.xw, pool + (size_t)p * G::C * G::CS, np.etab + (size_t)ca * 9 * G::C, np.head_w);
+          wave_lds_sync();
+          float x[G::AP], q[G::AP];
+          policy_logits<G>(W.xw, sm.t.hsc, x);
+          child_prior_regs<G>(sm.t, x, q, variant, W.fb, W.db);
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j)
+            if (lane + 64 * j < G::A) {
+              TV.prior[(size_t)cc * G::A + lane + 64 * j] = q[j];
+              TV.child[(size_t)cc * G::A + lane + 64 * j] = -1;
+            }
+          wave_lds_sync();
+        }
+      }
     }
+    __syncthreads();
+    for (int i = tid_local(); i < (G::TREE_CAP + 31) / 32; i += G::THREADS) sm.t.rawp[i] = 0u;
   }
   __syncthreads();
 }
@@ -2111,7 +2166,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const uint64_t key = stream_key(sp.seed, (uint32_t)(game_base + g), (uint32_t)move_index);
   run_search<G>(sm, np, sp, E, g, [&](int c, int j) { return o[c * G::CELLS + j]; },
                 noise ? noise + (size_t)g * G::A : nullptr, key);
-  settle_all_priors<G>(sm, TreeViewOf<G>::make(E, g), E.nodes[g], sp.variant);
+  settle_all_priors<G>(sm, np, E, g, E.nodes[g], sp.variant);
   search_outputs<G>(E, g, out_visits, out_value);
 }
 
@@ -2430,6 +2485,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
       }
   };
   if (E.status[g] != 0) { release_helpers(); tail_phase(); return; }
+  if ((sp.helpers > 0 || sp.tail) && tid_local() == 0)
+    __hip_atomic_store(job_of<G>(E_arg, g).started(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   BoardMeta m;
   load_board<G>(sm, E, g, m);

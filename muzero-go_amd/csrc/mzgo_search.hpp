@@ -46,8 +46,16 @@ struct TreeView {
 };
 
 // child-row entry 0 of a node whose prior row still holds its policy logits
-// (HBM trees: expand_child<LAZYH>; select_leaf settles it)
+// (the tower engine's HBM trees, k_texpand; select_leaf settles it)
 constexpr int kRawRow = -2;
+// child-row entry 0 of a batched child whose policy head was never computed
+// (the main engine's HBM trees: expand_child<LAZYH>, lazy policy head); its
+// prior row holds nothing until a select first reaches it
+constexpr int kLazyRow = -3;
+// select_leaf's result when its walk reached such a node (t.leaf) whose
+// policy sums are not in t.logits yet: the caller forms them (policy_sums_wg
+// from t.lpar's Y and E[t.lact]) and resumes the walk at t.leaf
+constexpr int kNeedLogits = -4;
 
 // Per-game LDS block used by the tree phases.
 template <class G>
@@ -65,7 +73,9 @@ struct TreeLds {
   int nunexp;              // select's leaf: number of unexpanded eligible children
   uint64_t umask[G::AP];   //   and their bitmask (a = 64 j + bit), the chosen one included
   int ycache;              // node whose Y the LDS copy holds (factored mode), -1: none
-  float hsc[64];                   // staged HeadScalars (HS_* offsets)
+  int lognode;             // node whose policy sums (no bias) logits[0..CELLS) holds (lazy head), -1: none
+  int lpar, lact;          // kNeedLogits: the parent and action of node t.leaf
+  float hsc[56];                   // staged HeadScalars (HS_* offsets, HS_COUNT of them)
   // LDS-resident tree state (boards with G::TREE_CAP > 0 and S + 2 <= TREE_CAP)
   int svis[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
   double sws[G::TREE_CAP > 0 ? G::TREE_CAP : 1];
@@ -88,8 +98,8 @@ struct TreeLds {
   float newp[G::A];
   int newest;              // id of the newest node (-1: none)
   int newp_node;           // node whose priors newp holds (atomic, workgroup scope)
-  // nodes whose prior row still holds the policy LOGITS (batched expansions
-  // of LDS trees: a row is turned into priors when a select first reaches the
+  // batched children whose policy head was never computed (LDS trees, lazy
+  // policy head: their prior rows are formed when a select first reaches the
   // node -- most children never are; see batch_expand)
   uint32_t rawp[G::TREE_CAP > 0 ? (G::TREE_CAP + 31) / 32 : 1];
   __device__ __forceinline__ bool is_raw(int n) const {
@@ -219,6 +229,7 @@ struct HeadScalars {
 // simulation): offsets into TreeLds::hsc.
 enum : int { HS_RB = 0, HS_FC1W = 1, HS_FC1B = 17, HS_FC2W = 33, HS_FC2B = 49, HS_VB = 50, HS_VFCW = 51,
              HS_VFCB = 52, HS_PB = 53, HS_PASS = 54, HS_COUNT = 55 };
+static_assert(HS_COUNT <= 56, "TreeLds::hsc holds the staged head scalars");
 
 // All threads; visible after the caller's next barrier.
 __device__ __forceinline__ void stage_head_scalars(const HeadScalars& hs, float* dst) {
@@ -415,25 +426,20 @@ __device__ __forceinline__ void child_priors(TreeLds<G>& t, const float (&x)[G::
     __hip_atomic_store(&t.newp_node, node, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// A raw prior row (policy logits, see TreeLds::rawp) -> the node's child
-// priors, in place; q gets them too.  A raw node has no children yet and its
-// child row was never written: crow gets -1s.  One wave; fbuf / dbuf: its
-// LDS scratch.
+// A lazily expanded node's child priors from its policy sums in t.logits
+// (policy_sums_wg): logits = sums + policy bias, pass logit last, then
+// child_priors' operations -> its prior row (in place), -1s into its child
+// row; q gets them too.  One wave; fbuf / dbuf: its LDS scratch.
 template <class G>
-__device__ __forceinline__ void settle_priors(TreeLds<G>& t, float* row, int* crow, int node, int variant,
-                                              float* fbuf, double* dbuf, float (&q)[G::AP]) {
+__device__ __forceinline__ void settle_lazy(TreeLds<G>& t, float* row, int* crow, int variant, float* fbuf,
+                                            double* dbuf, float (&q)[G::AP]) {
   const int lane = lane_id_local();
-#pragma unroll
-  for (int j = 0; j < G::AP; ++j)
-    if (lane + 64 * j < G::A) crow[lane + 64 * j] = -1;
   float x[G::AP];
-#pragma unroll
-  for (int j = 0; j < G::AP; ++j) x[j] = lane + 64 * j < G::A ? row[lane + 64 * j] : 0.f;
+  policy_logits<G>(t.logits, t.hsc, x);
   child_prior_regs<G>(t, x, q, variant, fbuf, dbuf);
 #pragma unroll
   for (int j = 0; j < G::AP; ++j)
-    if (lane + 64 * j < G::A) row[lane + 64 * j] = q[j];
-  if (lane == 0) atomicAnd(&t.rawp[node >> 5], ~(1u << (node & 31)));
+    if (lane + 64 * j < G::A) { row[lane + 64 * j] = q[j]; crow[lane + 64 * j] = -1; }
 }
 
 // The root's Gamma draws a = lane + 64 (w - 1) on waves w = 1..AP (one per
@@ -795,9 +801,16 @@ __device__ __forceinline__ int puct_pick(const double (&P)[G::AP], const int (&n
 // ---------------------------------------------------------------------------
 template <class G, class Acc>
 __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const SearchParams& sp,
-                                  uint64_t key, int sim, Stamp* st = nullptr) {
+                                  uint64_t key, int sim, Stamp* st = nullptr, int node0 = 0, int depth0 = 0) {
   const int lane = lane_id_local();
-  int node = 0, depth = 0;
+  // (node0, depth0): resume a walk that returned kNeedLogits at that node
+  int node = node0, depth = depth0, par = -1, pact = -1;
+  // a lazily expanded node reached for the first time: its policy sums
+  // first (the caller), unless t.logits holds them already
+  auto need_logits = [&]() {
+    t.leaf = node; t.depth = depth; t.lpar = par; t.lact = pact;
+    return kNeedLogits;
+  };
   for (int guard = 0; guard <= sp.num_simulations + 1; ++guard) {
     const bool root = node == 0;
     const int nvis = T.vis(node);
@@ -838,14 +851,15 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         P[j] = a < G::A ? (double)t.rowc_prior[a] : 0.0;
         ch[j] = a < G::A ? t.rowc_child[a] : -1;
       }
-    } else if (t.is_raw(node)) {               // first arrival: the row holds logits
+    } else if (t.is_raw(node)) {               // first arrival at a lazily expanded node
+      if (t.lognode != node) return need_logits();
       // t.fbuf / t.dbuf are wave 1's while it forms the newest node's priors
       if (t.newest >= 0)
         while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
           __builtin_amdgcn_s_sleep(1);
       float q[G::AP];
-      settle_priors<G>(t, const_cast<float*>(pr_row), T.T.child + (size_t)node * G::A, node, sp.variant, t.fbuf,
-                       t.dbuf, q);
+      settle_lazy<G>(t, const_cast<float*>(pr_row), T.T.child + (size_t)node * G::A, sp.variant, t.fbuf, t.dbuf, q);
+      if (lane == 0) atomicAnd(&t.rawp[node >> 5], ~(1u << (node & 31)));
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) {
         const int a = lane + 64 * j;
@@ -860,10 +874,25 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         ch[j] = a < G::A ? T.T.child[(size_t)node * G::A + a] : -1;
       }
       if constexpr (!Acc::LDS) {
-        // first arrival at a lazily expanded node (HBM trees): the row holds
-        // logits; turn it into priors in place (settle_priors without the
-        // LDS bit), its child row into -1s
-        if (__builtin_amdgcn_readfirstlane(ch[0]) == kRawRow) {
+        // first arrival at a lazily expanded node (HBM trees): its policy
+        // sums (kLazyRow) or the logits its row holds (kRawRow, the tower
+        // engine) -> priors in place, its child row -> -1s
+        const int c0 = __builtin_amdgcn_readfirstlane(ch[0]);
+        if (c0 == kLazyRow) {
+          if (t.lognode != node) return need_logits();
+          if (t.newest >= 0)                      // t.fbuf / t.dbuf: wave 1's while it forms newp
+            while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
+              __builtin_amdgcn_s_sleep(1);
+          float q[G::AP];
+          settle_lazy<G>(t, const_cast<float*>(pr_row), T.T.child + (size_t)node * G::A, sp.variant, t.fbuf,
+                         t.dbuf, q);
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            const int a = lane + 64 * j;
+            P[j] = a < G::A ? (double)q[j] : 0.0;
+            ch[j] = -1;
+          }
+        } else if (c0 == kRawRow) {
           if (t.newest >= 0)                      // t.fbuf / t.dbuf: wave 1's while it forms newp
             while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
               __builtin_amdgcn_s_sleep(1);
@@ -949,6 +978,8 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     if (root) t.ract = best_a;
     depth += 1;
     if (lane == 0) const_cast<Acc&>(T).set_path(depth, best_c);
+    par = node;
+    pact = best_a;
     node = best_c;
     if (st) {
       st->lap(depth == 1 ? 22 : 23);

@@ -1000,13 +1000,14 @@ struct TConvChain {
   unsigned long long* xcc;   // [nboards * co_chunks]: seq0 << 32 | XCC id of the launch
   unsigned seq0;
   int* err;
+  long long spin_max;        // bound of every wait in s_sleep rounds (1 << 24 ~ 1 s; a test hook may lower it)
 };
 
 // bounded wait until (int)(*p - want) >= 0 (thread 0); false on expiry
-__device__ __forceinline__ bool chain_wait(const unsigned* p, unsigned want) {
+__device__ __forceinline__ bool chain_wait(const unsigned* p, unsigned want, long long spin_max) {
   for (long long spins = 0; (int)(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0;
        ++spins) {
-    if (spins > (1ll << 24)) return false;
+    if (spins > spin_max) return false;
     __builtin_amdgcn_s_sleep(1);
   }
   return true;
@@ -1035,7 +1036,7 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c, const TConvAr
     for (int k = 0; k < CO; ++k) {
       unsigned long long v = __hip_atomic_load(xs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (long long spins = 0; (unsigned)(v >> 32) != c.seq0; ++spins) {
-        if (spins > (1ll << 24)) { bad = true; break; }
+        if (spins > c.spin_max) { bad = true; break; }
         __builtin_amdgcn_s_sleep(1);
         v = __hip_atomic_load(xs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1051,7 +1052,7 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c, const TConvAr
     if (l > 0) {
       // lanes 0..CO-1 of wave 0 poll the board's CO flags at once (one round trip each)
       if (threadIdx.x < (unsigned)CO && !bad) {
-        if (!chain_wait(fl + threadIdx.x, c.seq0 + (unsigned)l)) {
+        if (!chain_wait(fl + threadIdx.x, c.seq0 + (unsigned)l, c.spin_max)) {
           atomicOr(c.err, 1);
           bad = true;
         }

@@ -141,12 +141,17 @@ struct TowerHost {
       dev = c.dev;
       chains.push_back(std::move(c));
     }
-    const TConvChain ch{dev, (int)L.size(), cflags, cxcc, cseq, cerr};
+    // MZGO_TCONV_CHAIN_SPIN: the waits' bound (test hook: a tiny bound makes
+    // them expire, which every API call must then report)
+    long long spin_max = 1ll << 24;
+    if (const char* v = getenv("MZGO_TCONV_CHAIN_SPIN")) spin_max = atoll(v);
+    const TConvChain ch{dev, (int)L.size(), cflags, cxcc, cseq, cerr, spin_max};
     cseq += (unsigned)L.size();
     return ts->chain(ch, nb * CC, s);
   }
-  // a chain wait expired (results of that launch are wrong): read at the
-  // host's synchronisation points
+  // a chain wait expired (results of those launches are wrong): read (and
+  // cleared, once reported) at every host synchronisation point of the
+  // tower engine's API calls (mzgo_check_chain)
   hipError_t chain_error(hipStream_t s, bool& bad) {
     bad = false;
     if (!cerr) return hipSuccess;
@@ -154,6 +159,8 @@ struct TowerHost {
     hipError_t e = hipMemcpyAsync(&v, cerr, sizeof(int), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     bad = v != 0;
+    if (bad && e == hipSuccess) e = hipMemsetAsync(cerr, 0, sizeof(int), s);
+    if (bad && e == hipSuccess) e = hipStreamSynchronize(s);
     return e;
   }
   void free_chains() {

@@ -13,6 +13,7 @@ self_play.py), all executed by libmzgo.so's HIP kernels:
 * ``GameHistory``, ``save_batches`` -- the reference's record / pickle format
 * ``mzgo.play`` -- play.py's interactive human-vs-agent loop (``python -m mzgo.play weights.pth``)
 """
+from ._lib import MzgoError
 from .arena import SelfPlayEvaluator
 from .engine import Engine, EngineConfig
 from .env import GoEnv
@@ -24,4 +25,4 @@ from .weights import deterministic_res_state_dict, deterministic_state_dict
 
 __all__ = ["Engine", "EngineConfig", "GoEnv", "MuZeroNet", "MCTS", "MainMCTS", "MuZeroAgent", "SelfPlay",
            "GameHistory", "history_from_device", "save_batches", "deterministic_state_dict", "SelfPlayEvaluator",
-           "ResMuZeroNet", "deterministic_res_state_dict"]
+           "ResMuZeroNet", "deterministic_res_state_dict", "MzgoError"]

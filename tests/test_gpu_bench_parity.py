@@ -280,3 +280,36 @@ def test_tail_helpers_do_not_change_records(epoch, monkeypatch):
     assert {k: v for k, v in ca.items() if k != "tail_convs"} == {k: v for k, v in cb.items() if k != "tail_convs"}
     for k in aa:
         np.testing.assert_array_equal(aa[k].view(np.uint8), ab[k].view(np.uint8), err_msg=k)
+
+
+@pytest.mark.timeout(300)
+def test_tail_helpers_games_above_cu_count(monkeypatch):
+    """More games than CUs (9x9: one workgroup per CU): the host leaves the
+    epoch tail off by default -- ended workgroups would hold CUs that games
+    not yet dispatched wait for (tail_enabled) --; forced on
+    (MZGO_TAIL_HELPERS=2) the kernel's own guards (a helper joins only games
+    whose workgroup has started, and exits when its bounded wait expires)
+    still finish the launch, with records byte-identical to the tail off."""
+    import mzgo
+    N, S = 9, 8
+    G = torch.cuda.get_device_properties(0).multi_processor_count + 44
+    net = _net(N)
+    sp = mzgo.SelfPlay(net, G, S, seed=SEED)
+    eng = sp.engine
+    out = {}
+    for mode in ("1", "2", "0"):
+        monkeypatch.setenv("MZGO_TAIL_HELPERS", mode)
+        c0 = eng.counters()
+        sp.reset(epoch=2)
+        sp.move(sp.max_moves)
+        c1 = eng.counters()
+        recs, arrays = _records(eng)
+        out[mode] = (arrays, {k: c1[k] - c0[k] for k in c1 if k != "playing"})
+    assert out["1"][1]["tail_convs"] == 0 and out["0"][1]["tail_convs"] == 0, (out["1"][1], out["0"][1])
+    assert out["1"][1]["games_finished"] == G
+    for mode in ("1", "2"):
+        a, c = out[mode]
+        assert {k: v for k, v in c.items() if k != "tail_convs"} == \
+            {k: v for k, v in out["0"][1].items() if k != "tail_convs"}
+        for k in a:
+            np.testing.assert_array_equal(a[k].view(np.uint8), out["0"][0][k].view(np.uint8), err_msg=f"{mode} {k}")

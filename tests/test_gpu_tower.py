@@ -373,3 +373,23 @@ def test_tower_chain_launch_equals_per_conv_launches(monkeypatch):
     for a, b in zip(ta, tb):
         for k in a:
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+
+
+def test_tower_chain_wait_expiry_is_reported(monkeypatch):
+    """An expired k_tconv_chain wait (the launch's results are wrong) is
+    reported by the API call that made it -- here a single move() -- as
+    MZGO_EHIP, and cleared: the next calls succeed.  The expiry is forced by
+    the test hook MZGO_TCONV_CHAIN_SPIN=-1 (every wait gives up at once)."""
+    import mzgo
+    N, C, blocks, G, S = 9, 128, 1, 8, 8
+    net = _nets(N, C, blocks, seed=3)[0]
+    sp = mzgo.SelfPlay(net, G, S, seed=5)
+    sp.reset()
+    monkeypatch.setenv("MZGO_TCONV_CHAIN_SPIN", "-1")
+    with pytest.raises(mzgo.MzgoError, match="k_tconv_chain"):
+        sp.move()
+    monkeypatch.delenv("MZGO_TCONV_CHAIN_SPIN")
+    sp.engine.counters()
+    sp.reset()
+    sp.move()
+    assert sp.engine.counters()["moves"] >= G
