@@ -124,16 +124,17 @@ PEAK_FP32_MFMA_TFLOPS = 157.3
 CUS, PEAK_CLK_GHZ = 256, 2.4
 
 
-def pmc_summary(workload, dynamics, moves_per_launch):
+def pmc_summary(workload, dynamics, moves_per_launch, n_gpus=1):
     """Per-launch PMC means of k_selfplay_move from rocprofv3 passes of this
     same bench command (scripts/pmc.sh -> profiles/<tag>_pmc.json);
-    only a profile of the same workload and launch structure counts."""
+    only a profile of the same workload, launch structure and GPU count
+    counts (the passes are 1-GPU runs: an N > 1 line gets none)."""
     import glob
     for path in [os.path.join(ROOT, "profiles", "latest_pmc.json")] + \
             sorted(glob.glob(os.path.join(ROOT, "profiles", "latest_pmc_*.json"))):
         p = json.load(open(path))
         if (p.get("workload") == workload and p.get("dynamics") == dynamics
-                and p.get("moves_per_launch", 1) == moves_per_launch):
+                and p.get("moves_per_launch", 1) == moves_per_launch and p.get("n_gpus", 1) == n_gpus):
             return p
     return None
 
@@ -167,7 +168,7 @@ def phases_summary(workload, moves_per_launch):
     return out
 
 
-def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch):
+def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch, n_gpus=1):
     """Roofline of the dominant kernel, k_selfplay_move, per launch.
 
     Executed MFMA work: the dynamics convs the searches ran (Winograd GEMMs at
@@ -186,12 +187,15 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
     mfma_tf = mfma_l / avg_kern_s / 1e12
     CS = (CELLS + 15) // 16 * 16
     if dynamics == "factored":
-        # per simulation the new node's prior (logit) row written; per conv its
-        # input read (the parent's Y, or the root latent: the rebuilt latent is
+        # per prior row formed (engine counter: eager expansions, and lazily
+        # expanded nodes a select reached -- the lazy policy head writes no row
+        # for the others) the node's prior and child rows; per conv its input
+        # read (the parent's Y, or the root latent: the rebuilt latent is
         # formed inside the input transform, never stored) and its Y written;
         # per move the representation's three conv outputs (64, 64, C channels)
         # written and read back, and the record (planes, policy, scalars)
-        hbm_l = (sims_l * A * 4 + convs_l * 2 * CELLS * C * 4
+        rows_l = counts.get("rows", counts["sims"]) / L
+        hbm_l = (rows_l * 2 * A * 4 + convs_l * 2 * CELLS * C * 4
                  + moves_l * (2 * (128 + C) * CS * 4 + 2 * CELLS + A * 8 + 32))
     else:
         hbm_l = sims_l * (2 * C * CS * 4 + A * 4) + moves_l * ((6 * CELLS + 2 * C * CS) * 4 + A * 8)
@@ -204,7 +208,7 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
                 "what": "algorithmic HBM bytes of the factored search (E[a] table and weights L2-resident, "
                         "not charged; a parent's Y read from the LDS copy still charged)"},
     }
-    pmc = pmc_summary(workload, dynamics, moves_per_launch)
+    pmc = pmc_summary(workload, dynamics, moves_per_launch, n_gpus)
     traffic = None
     if pmc is not None:
         c = pmc["counters"]
@@ -232,7 +236,8 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
     return {"bound": bound, "kernel": "k_selfplay_move", "achieved": u["achieved"], "peak": u["peak"],
             "unit": u["unit"], "frac": u["frac"], "traffic": traffic,
             "avg_launch_ms": avg_kern_s * 1e3, "sims_per_launch": sims_l,
-            "dynamics_convs_per_move": convs_l / max(moves_l, 1e-9), "units": units,
+            "dynamics_convs_per_move": convs_l / max(moves_l, 1e-9),
+            "prior_rows_per_move": counts.get("rows", counts["sims"]) / L / max(moves_l, 1e-9), "units": units,
             "algorithm": "factored dynamics (conv once per parent, children relu(Y + E[a])), batched + "
                          "replayed expansions" if dynamics == "factored" else
                          "a Winograd / implicit-GEMM dynamics conv per simulation"}
@@ -443,6 +448,7 @@ def refill_main(args, net, world, rank, local, cpu_ref):
     sims = sum(b["simulations"] - a["simulations"] for a, b in zip(c0, c1))
     moves = sum(b["moves"] - a["moves"] for a, b in zip(c0, c1))
     convs = sum(b["dynamics_convs"] - a["dynamics_convs"] for a, b in zip(c0, c1))
+    rows = sum(b["prior_rows"] - a["prior_rows"] for a, b in zip(c0, c1))
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     if world > 1:
         t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64,
@@ -453,11 +459,11 @@ def refill_main(args, net, world, rank, local, cpu_ref):
         dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
     if rank == 0:
         workload = f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move"
-        counts = dict(launches=len(kern_ms), sims=sims / world, moves=moves / world, convs=convs)
+        counts = dict(launches=len(kern_ms), sims=sims / world, moves=moves / world, convs=convs, rows=rows)
         # R engines' epochs overlap on R streams, so an epoch's own event span
         # includes the time it shares the GPU: the roofline is taken on wall
         # time instead (all epochs' work / dt, i.e. dt / epochs per launch)
-        roof = roofline(N, C, S, G, counts, dt / len(kern_ms), args.dynamics, workload + f", refill {R}", 0)
+        roof = roofline(N, C, S, G, counts, dt / len(kern_ms), args.dynamics, workload + f", refill {R}", 0, world)
         roof["avg_launch_ms_basis"] = "wall time / epochs (overlapping streams)"
         roof["epoch_event_span_ms"] = sum(kern_ms) / len(kern_ms)
         out = {
@@ -532,11 +538,19 @@ def main():
         if getattr(args, k) is None:
             setattr(args, k, v)
 
+    blocks = args.blocks if args.config == 5 else None
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # --gpus N without a launcher: N fresh rank processes (RANK / LOCAL_RANK /
         # WORLD_SIZE / MASTER_* as torch.distributed.run sets them), started
         # before anything here loads libmzgo.so or touches a GPU; rank 0 prints
-        # the line, this process exits with the ranks' status
+        # the line, this process exits with the ranks' status.  The CPU
+        # baseline runs here first (this process never touches a GPU) and
+        # reaches rank 0's line through the environment.
+        if not args.no_cpu_baseline:
+            ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget, args.cpu_procs,
+                                     blocks)
+            ref["measured_in"] = "launcher process, before the ranks started (no GPU work running)"
+            os.environ["MZGO_CPU_BASELINE"] = json.dumps(ref)
         sys.exit(_launch_module().spawn_ranks(
             args.gpus, [sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -552,10 +566,17 @@ def main():
     if os.environ.get("MZGO_SHARE_DEVICE") == "1":
         local = 0
     cpu_ref = None
-    if world == 1 and not args.no_cpu_baseline:
-        # before the GPU is initialised: the baseline spawns worker processes
-        cpu_ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget, args.cpu_procs,
-                                     args.blocks if args.config == 5 else None)
+    if rank == 0 and not args.no_cpu_baseline:
+        if "MZGO_CPU_BASELINE" in os.environ:        # (bench.py --gpus N's own launcher measured it)
+            cpu_ref = json.loads(os.environ["MZGO_CPU_BASELINE"])
+        else:
+            # before the GPU is initialised (the baseline spawns worker
+            # processes); under torch.distributed.run the other ranks wait for
+            # rank 0 in init_process_group meanwhile
+            cpu_ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget,
+                                         args.cpu_procs, blocks)
+            if world > 1:
+                cpu_ref["measured_in"] = "rank 0, before GPU initialisation (the other ranks waiting)"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -616,16 +637,32 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    gathers = []
+    # The trajectory gather of config 3 (RCCL, the only collective on the
+    # data path): every timed epoch's records are packed on the device into
+    # their own slice of a rank-local HBM staging buffer (a D2D copy on the
+    # launch stream, 17 MB per epoch at 9x9 / 256 games), and the staged
+    # epochs go to rank 0's HBM in ONE gather at the end of the timed loop.
+    # A gather per epoch would share the chip with the next epoch: RCCL moves
+    # data with kernels, an epoch puts one workgroup on every CU at ~159 KiB
+    # of LDS, and a collective kernel resident while it waits for the
+    # slowest rank displaces a game's workgroup for that long -- measured
+    # with a stand-in kernel waiting 20 ms: +11 ms per 49 ms epoch overlapped,
+    # +2.4 ms even when gated until the next epoch is resident
+    # (scripts/rccl_standin.py).  One large collective at the end
+    # never overlaps an epoch, and 288 GB of HBM holds the staging easily.
+    gathers, staged = [], None
+    if world > 1:
+        per_epoch = mdist.pack_engine(eng).numel()
+        staged = torch.empty(args.steps * per_epoch, dtype=torch.uint8, device=f"cuda:{local}")
+        torch.cuda.synchronize()
+
     t0 = time.perf_counter()
     for i in range(args.steps):
         one_epoch(ev[i])
         if world > 1:
-            # the trajectory gather of config 3: after every epoch, every rank's
-            # packed game records to rank 0's HBM over RCCL (the only collective
-            # on the data path); asynchronous, so the next epoch's launch is
-            # queued at once and the gather runs on RCCL's stream beside it
-            gathers.append(mdist.gather_packed(mdist.pack_engine(eng), async_op=True))
+            mdist.pack_engine(eng, out=staged[i * per_epoch:(i + 1) * per_epoch])
+    if world > 1:
+        gathers.append(mdist.gather_packed(staged, async_op=True))
     for work, _ in gathers:
         work.wait()
     torch.cuda.synchronize()
@@ -652,8 +689,9 @@ def main():
     if rank == 0:
         workload = f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move"
         counts = dict(launches=launches, sims=sims / world, moves=moves / world,
-                      convs=(c1["dynamics_convs"] - c0["dynamics_convs"]))
-        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload, args.moves_per_launch)
+                      convs=(c1["dynamics_convs"] - c0["dynamics_convs"]),
+                      rows=(c1["prior_rows"] - c0["prior_rows"]))
+        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload, args.moves_per_launch, world)
         out = {
             "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {S} sims/move",
             "value": sims / dt,
@@ -677,9 +715,14 @@ def main():
             "roofline": roof,
         }
         if world > 1:
-            out["gather"] = {"collective": f"{dist.get_backend()} gather to rank 0", "per_step": 1,
-                             "count": len(gathers), "bytes_per_rank": int(gathers[0][1][0].numel()) if gathers else 0}
-        ph = phases_summary(workload, args.moves_per_launch) if args.dynamics == "factored" else None
+            out["gather"] = {"collective": f"{dist.get_backend()} gather to rank 0", "count": len(gathers),
+                             "epochs_per_gather": args.steps, "bytes_per_rank": int(staged.numel()),
+                             "bytes_per_epoch_per_rank": int(per_epoch),
+                             "schedule": "every timed epoch's records packed into a rank-local HBM staging slice; "
+                                         "one gather of all of them at the end of the timed loop (inside it): no "
+                                         "collective kernel shares the chip with an epoch"}
+        # (the stamps build is profiled on one GPU: phase shares only on 1-GPU lines)
+        ph = phases_summary(workload, args.moves_per_launch) if args.dynamics == "factored" and world == 1 else None
         if ph is not None:
             out["phases"] = ph
         if cpu_ref is not None:

@@ -142,12 +142,17 @@ int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uin
 
 /* Self-play.  selfplay_reset starts a new game in every slot (epoch = RNG
  * generation of the games); selfplay_move plays one move in every unfinished
- * slot.  selfplay_counters (host u64 [6], synchronises; cumulative over the
+ * slot.  selfplay_counters (host u64 [8], synchronises; cumulative over the
  * engine's life): [0] simulations run, [1] moves played, [2] games finished,
  * [3] slots still playing now, [4] dynamics 3x3 convs run by searches (one per
  * expansion with direct_dynamics, one per new parent node when factored),
  * [5] of those, parent convs shared with the workgroups of games that had
- * already ended (9x9 whole-game launches: the epoch tail). */
+ * already ended (9x9 whole-game launches: the epoch tail), [6] prior rows
+ * formed by searches (a node's child priors + child row written to HBM: every
+ * eagerly expanded child, and a lazily expanded one -- the lazy policy head --
+ * only when a select first reaches it; 0 on tower engines), [7] self-play
+ * game workgroups started (every slot's workgroup of every launch counts one
+ * when it begins: mzgo_stream_wait_started's count). */
 int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
 /* Up to ``moves`` consecutive moves of every unfinished slot in ONE launch
@@ -157,7 +162,8 @@ int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
  * moves > 4 they read the slots' status every 4 moves (BLOCKING: the stream is
  * synchronised there, so such a call cannot be captured in a HIP graph) and
  * stop enqueueing once every game has ended -- the same records and counters
- * as ``moves`` single-move calls.  moves <= 4 never synchronises. */
+ * as ``moves`` single-move calls -- and synchronise once at the end of every
+ * call, which reports an expired k_tconv_chain wait (MZGO_EHIP). */
 int mzgo_selfplay_moves(mzgo_engine* eng, int moves, void* stream);
 
 /* Arena (main.py:526-611, SelfPlayEvaluator): like mzgo_selfplay_move, but
@@ -171,6 +177,14 @@ int mzgo_arena_move(mzgo_engine* eng, mzgo_engine* opponent, void* stream);
 /* ``moves`` arena moves per slot in one launch (as mzgo_selfplay_moves). */
 int mzgo_arena_moves(mzgo_engine* eng, mzgo_engine* opponent, int moves, void* stream);
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
+/* Enqueue on ``stream`` a gate that completes once counter [7] (self-play
+ * workgroups started) reaches ``target``: work queued behind it -- a
+ * collective -- cannot take a CU before every workgroup of the self-play
+ * launch that brings the count to target is resident (a self-play workgroup
+ * fills a CU's LDS).  The gate itself is one wave without LDS, so it sits
+ * beside them; its wait is bounded (~seconds).  bench.py --gpus N gates each
+ * epoch's record gather on the next epoch's launch this way. */
+int mzgo_stream_wait_started(mzgo_engine* eng, uint64_t target, void* stream);
 /* Tower engines (tower = 1): report (synchronising) and reset the time spent
  * in the dynamics towers since the last call -- one HIP event pair around each
  * simulation step's 2*res_blocks+1 conv launches, on the launch stream -- then
@@ -214,6 +228,18 @@ int mzgo_conv3x3_backward(const float* grad_out, const float* out, const float* 
  * caller-owned, must outlive the moves) instead of the counter-RNG sampler;
  * NULL restores sampling. */
 int mzgo_selfplay_inject_noise(mzgo_engine* eng, const double* noise);
+/* Test hook (parity of the sampled-noise path): every self-play root's
+ * normalised Dirichlet sample -- the one the counter-RNG sampler drew, or the
+ * injected one -- written to dst f64 [G][max_moves][A] (device, caller-owned,
+ * must outlive the moves) at (slot, move); NULL turns it off. */
+int mzgo_selfplay_record_noise(mzgo_engine* eng, double* dst);
+/* Test hook, tower engines (tower = 1): every node the searches evaluate,
+ * written to dst f32 [G][S+1][A+2] (device, caller-owned) at (slot, node id)
+ * as the tower produced it: the policy logits [A], then reward and value
+ * (node 0: the representation's logits and value, reward 0).  With it a
+ * CPU search driven by these outputs must rebuild the device tree exactly.
+ * NULL turns it off. */
+int mzgo_tower_record_nodes(mzgo_engine* eng, float* dst);
 
 /* Copy slot g's game record to host buffers (synchronises ``stream``).
  * length: moves recorded; ended: 1 if the game ended by double pass; status.

@@ -204,6 +204,7 @@ struct mzgo_engine {
   int64_t bytes = 0;
   int epoch = 0;
   const double* noise = nullptr;
+  double* noise_out = nullptr;  // test hook: roots' normalised Dirichlet samples [G][M][A]
   TowerHost* tower = nullptr;   // residual-tower network (mzgo_config.tower, BASELINE config 5)
 
   template <class T>
@@ -468,14 +469,14 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   chk(e->alloc(&E.game_len, G));
   chk(e->alloc(&E.final_reward, G));
   chk(e->alloc(&E.status, G));
-  chk(e->alloc(&E.counters, 5));
+  chk(e->alloc(&E.counters, 7));
   chk(e->alloc(&e->d_err, 1));
 #ifdef MZGO_STAMPS
   chk(e->alloc(&E.stamps, G * kStampPhases));
   if (E.stamps) (void)hipMemset(E.stamps, 0, G * kStampPhases * 8);
 #endif
   if (rc != MZGO_OK) { delete e; return rc; }
-  if (hipMemset(E.counters, 0, 5 * sizeof(unsigned long long)) != hipSuccess ||
+  if (hipMemset(E.counters, 0, 7 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess) {
     delete e;
     return fail(MZGO_EHIP, "hipMemset failed");
@@ -743,6 +744,7 @@ int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
   pp.game_base = e->cfg.game_base;
   pp.epoch = e->epoch;
   pp.noise = e->noise;
+  pp.noise_out = e->noise_out;
   pp.arena = 0;
   pp.moves = moves;
   if (e->tower) {
@@ -797,6 +799,7 @@ int mzgo_arena_moves(mzgo_engine* e, mzgo_engine* opponent, int moves, void* str
   pp.game_base = e->cfg.game_base;
   pp.epoch = e->epoch;
   pp.noise = e->noise;
+  pp.noise_out = e->noise_out;
   pp.arena = 1;
   pp.moves = moves;
   return launch_selfplay(e, opponent->np, pp, (hipStream_t)stream);
@@ -871,10 +874,23 @@ int mzgo_selfplay_inject_noise(mzgo_engine* e, const double* noise) {
   return MZGO_OK;
 }
 
+int mzgo_selfplay_record_noise(mzgo_engine* e, double* dst) {
+  if (!e) return fail(MZGO_EINVAL, "null engine");
+  if (e->tower) return fail(MZGO_EINVAL, "the noise record covers the reference-network engine (tower 0)");
+  e->noise_out = dst;
+  return MZGO_OK;
+}
+
+int mzgo_tower_record_nodes(mzgo_engine* e, float* dst) {
+  if (!e || !e->tower) return fail(MZGO_EINVAL, "not a tower engine");
+  e->tower->TA.node_out = dst;
+  return MZGO_OK;
+}
+
 int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   if (!e || !out) return fail(MZGO_EINVAL, "bad argument");
   hipStream_t s = (hipStream_t)stream;
-  unsigned long long c[5] = {0, 0, 0, 0, 0};
+  unsigned long long c[7] = {0, 0, 0, 0, 0, 0, 0};
   std::vector<int> st(e->G);
   HIPCHK(hipMemcpyAsync(c, e->E.counters, sizeof c, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -883,6 +899,7 @@ int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   int playing = 0;
   for (int v : st) playing += v == 0;
   out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing; out[4] = c[3]; out[5] = c[4];
+  out[6] = c[5]; out[7] = c[6];
   return MZGO_OK;
 }
 
@@ -924,6 +941,25 @@ int mzgo_debug_stamps(mzgo_engine* e, unsigned long long* host) {
   return MZGO_OK;
 }
 #endif
+
+// A gate for a collective (mzgo_stream_wait_started): one wave, no LDS and a
+// handful of registers, so it sits beside a self-play workgroup on any CU;
+// it returns once *count >= target (or after a bounded ~seconds wait)
+__global__ void __launch_bounds__(64) k_wait_count(const unsigned long long* count, unsigned long long target) {
+  if (threadIdx.x != 0) return;
+  for (long long spins = 0; spins < (1ll << 26); ++spins) {
+    if (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+    __builtin_amdgcn_s_sleep(16);
+  }
+}
+
+int mzgo_stream_wait_started(mzgo_engine* e, uint64_t target, void* stream) {
+  if (!e || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  hipLaunchKernelGGL(k_wait_count, dim3(1), dim3(64), 0, (hipStream_t)stream, e->E.counters + 6,
+                     (unsigned long long)target);
+  HIPCHK(hipGetLastError());
+  return MZGO_OK;
+}
 
 // Packed records of all G slots, for the multi-GPU gather (layout in mzgo.h).
 int mzgo_records_pack(mzgo_engine* e, uint8_t* dst, int64_t capacity, int64_t* bytes_needed, void* stream) {

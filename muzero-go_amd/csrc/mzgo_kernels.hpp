@@ -91,9 +91,10 @@ struct EngineArrays {
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
   unsigned char* jobs;   // [G][job_bytes(A)] batch-expansion jobs shared with helper workgroups
-  unsigned long long* counters;  // [5] 0: simulations run, 1: moves played, 2: games finished,
+  unsigned long long* counters;  // [7] 0: simulations run, 1: moves played, 2: games finished,
                                  //     3: dynamics convs run (factored: one per new parent),
-                                 //     4: of those, tail conv jobs (conv_tail)
+                                 //     4: of those, tail conv jobs (conv_tail), 5: prior rows formed,
+                                 //     6: game workgroups started (k_selfplay_move)
   unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
 };
 
@@ -1760,10 +1761,14 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   __syncthreads();
 
   int nodes = 1, convs = 0;
+  // prior rows formed (HBM writes of a node's priors + child row): eager
+  // expansions, and lazily expanded nodes on a select's first arrival
+  int rows = 0;
   Stamp st(E.stamps);
   int sim = 0;
   if (factored) {
     sim = root_batch<G, Acc>(sm, np, sp, E, g, TV, T, pool, scratch, nact, key, &st);
+    if (!(Acc::LDS || shared_jobs<G>(sp))) rows += sim;
     nodes += sim;
     convs += sim > 0 ? 1 : 0;
     st.lap(4);
@@ -1788,6 +1793,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       policy_sums_wg<G>(sm.t.logits, pool + (size_t)sm.t.lpar * node_floats,
                         np.etab + (size_t)sm.t.lact * 9 * G::C, np.head_w);
       if (tid_local() == 0) sm.t.lognode = xn;
+      ++rows;
       __syncthreads();
       if (wave_id() == 0) {
         const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st, xn, xd);
@@ -1935,6 +1941,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         }
         __syncthreads();
         st.lap(5);
+        if (!(Acc::LDS || shared_jobs<G>(sp))) rows += B;
         if (depth <= kVerifyMaxDepth && replay_parallel(shared_jobs<G>(sp), B, depth)) {
           const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st, shared_jobs<G>(sp));
           nodes += m;
@@ -1996,6 +2003,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       const unsigned long long t_x = st.now();
       expand_heads<G>(sm.u.f, yleaf, yc == leaf, np.etab + (size_t)a * 9 * G::C, np.head_w);
       if (tid_local() == 0) st.wave_add(56, st.now() - t_x);
+      ++rows;
       __syncthreads();
       if (tid_local() == 0 && decltype(sm.u.f)::CACHE) sm.t.ycache = leaf;   // read by all before the barrier
       heads = sm.u.f.xh;
@@ -2042,6 +2050,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     E.nodes[g] = nodes;
     // direct dynamics: one conv per expansion
     atomicAdd(&E.counters[3], (unsigned long long)(factored ? convs : nodes - 1));
+    atomicAdd(&E.counters[5], (unsigned long long)(factored ? rows : nodes - 1));
   }
   __syncthreads();
 }
@@ -2049,7 +2058,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
 template <class G, class PlaneFn>
 __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, const SearchParams& sp,
                                   const EngineArrays& E, int g, PlaneFn planes, const double* noise,
-                                  uint64_t key, unsigned long long* ts = nullptr) {
+                                  uint64_t key, unsigned long long* ts = nullptr, double* noise_out = nullptr) {
   const TreeView TV = TreeViewOf<G>::make(E, g);
   if (tid_local() == 0) sm.t.ngrab = 0;             // draw_dirichlet's counter (build_mask's barrier orders it)
   build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return planes(3, a); });
@@ -2068,11 +2077,11 @@ __device__ __forceinline__ void run_search(Smem<G>& sm, const NetParams& np, con
   if (ts) ts[0] = __builtin_amdgcn_s_memtime();
 #endif
   if (noise) {
-    if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key);
+    if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key, nullptr, noise_out);
   } else {
     static_assert(G::AP < G::WAVES, "a wave per 64 Gamma draws besides wave 0");
     draw_dirichlet<G>(sm.t, key, sp.dirichlet_alpha, &sm.t.ngrab);
-    if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key, &sm.t.ngrab);
+    if (wave_id() == 0) root_priors<G>(sm.t, TV, sp, noise, key, &sm.t.ngrab, noise_out);
   }
   __syncthreads();
 #ifdef MZGO_STAMPS
@@ -2424,6 +2433,7 @@ struct PlayParams {
   int game_base;          // global id of slot 0 (multi-GPU sharding)
   int epoch;              // game generation (slot restarts), part of the RNG key
   const double* noise;    // test hook: injected Dirichlet samples [G][M][A], or null
+  double* noise_out;      // test hook: every root's normalised Dirichlet sample [G][M][A], or null
   int arena;              // 0: one network; 1: main.py's evaluator -- game i's first
                           // mover is network (i % 2), then the networks alternate
   int moves;              // moves per game in this launch (each game stops at its end)
@@ -2456,6 +2466,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   }
   const int g = blockIdx.x;
   const EngineArrays& E = E_arg;
+  // (every game workgroup counts itself resident: mzgo_stream_wait_started)
+  if (tid_local() == 0) atomicAdd(&E_arg.counters[6], 1ull);
   auto release_helpers = [&]() {
     if ((sp.helpers > 0 || sp.tail) && tid_local() == 0)
       __hip_atomic_store(job_of<G>(E_arg, g).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2525,13 +2537,14 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
   const BoardMeta m0 = m;
   const double* noise = pp.noise ? pp.noise + ((size_t)g * E.max_moves + mv) * G::A : nullptr;
+  double* noise_out = pp.noise_out ? pp.noise_out + ((size_t)g * E.max_moves + mv) * G::A : nullptr;
 #ifdef MZGO_STAMPS
   tm[1] = __builtin_amdgcn_s_memtime();
 #endif
   SearchParams spm = sp;
   spm.net = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? 1 : 0;
   run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
-                tm ? tm + 2 : nullptr);
+                tm ? tm + 2 : nullptr, noise_out);
 #ifdef MZGO_STAMPS
   tm[4] = __builtin_amdgcn_s_memtime();
 #endif

@@ -478,10 +478,12 @@ __device__ __forceinline__ void draw_dirichlet(TreeLds<G>& t, uint64_t key, doub
 }
 
 // Root priors (self_play.py:151-182) into T.root_prior.  noise: injected
-// Dirichlet sample [A] (nullable: sample from the counter stream).  Wave 0.
+// Dirichlet sample [A] (nullable: sample from the counter stream); noise_out
+// (test hook, nullable): the normalised sample used [A].  Wave 0.
 template <class G>
 __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, const SearchParams& sp,
-                                   const double* noise, uint64_t key, int* drawn = nullptr) {
+                                   const double* noise, uint64_t key, int* drawn = nullptr,
+                                   double* noise_out = nullptr) {
   const int lane = lane_id_local();
   softmax_wave<G>(t);
   for (int a = lane; a < G::A; a += 64) t.fbuf[a] = mul_f32_by_f64(t.fbuf[a], mask_of<G>(t, a));
@@ -500,6 +502,8 @@ __device__ __forceinline__ void root_priors(TreeLds<G>& t, const TreeView& T, co
     const double gs = np_pairwise_sum<double, G::A>(t.dbuf);
     for (int a = lane; a < G::A; a += 64) t.dbuf[a] = gs > 0 ? t.dbuf[a] / gs : 1.0 / G::A;
   }
+  if (noise_out)
+    for (int a = lane; a < G::A; a += 64) noise_out[a] = t.dbuf[a];
   const double eps = sp.dirichlet_epsilon;
   const float keep32 = (float)(1.0 - eps);   // Python float * f32 array -> f32 (NEP 50)
   if (sp.variant == 1) {

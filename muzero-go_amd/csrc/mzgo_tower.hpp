@@ -1102,6 +1102,7 @@ struct TowerArrays {
   int C, co_chunks;
   HeadScalars hs;
   const float* headw;    // [3][C]: reward_conv, value_conv, policy_conv
+  float* node_out;       // test hook (mzgo_tower_record_nodes): [G][S+1][A+2] logits, reward, value; or null
 };
 
 template <class G>
@@ -1246,6 +1247,13 @@ __global__ void __launch_bounds__(64) k_troot(TowerArrays T, SearchParams sp, En
   // representation: no reward head; value, then policy (rows 1, 2 of hp)
   heads_logits<G, 1>(hp + G::CS, false, t.hsc, t.logits);
   wave_lds_sync();
+  if (T.node_out) {                       // (test hook) node 0: the root's logits and value
+    float* o = T.node_out + (size_t)g * (E.S + 1) * (G::A + 2);
+    float r, v;
+    heads_value<G, 1>(hp + G::CS, false, t.hsc, r, v);
+    for (int a = threadIdx.x; a < G::A; a += 64) o[a] = t.logits[a];
+    if (threadIdx.x == 0) { o[G::A] = 0.f; o[G::A + 1] = v; }
+  }
   const TreeView TV = TreeViewOf<G>::make(E, g);
   // injected Dirichlet samples (test hook): [G][A] (search) or [G][M][A] (self-play)
   const double* nz = noise ? noise + (size_t)g * game_stride + (per_move ? (size_t)E.meta[g * 4 + 3] * G::A : 0)
@@ -1315,6 +1323,13 @@ __global__ void __launch_bounds__(64) k_texpand(TowerArrays T, SearchParams sp, 
     for (int j = 0; j < G::AP; ++j)
       if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
     if (lane == 0) TV.child[(size_t)nid * G::A] = kRawRow;
+    if (T.node_out) {                     // (test hook) the node as the tower evaluated it
+      float* o = T.node_out + ((size_t)g * (E.S + 1) + nid) * (G::A + 2);
+#pragma unroll
+      for (int j = 0; j < G::AP; ++j)
+        if (lane + 64 * j < G::A) o[lane + 64 * j] = x[j];
+      if (lane == 0) { o[G::A] = r; o[G::A + 1] = v; }
+    }
   }
   if (threadIdx.x == 0) acc.init(nid);
   if (threadIdx.x == (a & 63)) acc.set_child(leaf, a, nid);

@@ -71,8 +71,11 @@ SIGNATURES = {
     "mzgo_arena_move": (_I, [_P, _P, _P]),
     "mzgo_arena_moves": (_I, [_P, _P, _I, _P]),
     "mzgo_selfplay_counters": (_I, [_P, _P, _P]),
+    "mzgo_stream_wait_started": (_I, [_P, ctypes.c_uint64, _P]),
     "mzgo_tower_timing": (_I, [_P, _I, _P, _P]),
     "mzgo_selfplay_inject_noise": (_I, [_P, _P]),
+    "mzgo_selfplay_record_noise": (_I, [_P, _P]),
+    "mzgo_tower_record_nodes": (_I, [_P, _P]),
     "mzgo_records_export": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mzgo_records_pack": (_I, [_P, _P, ctypes.c_int64, _P, _P]),
     "mzgo_dyn_conv_backward_workspace": (_I, [_I, _I, ctypes.POINTER(ctypes.c_int64)]),

@@ -59,14 +59,18 @@ def slot_records(arrays, g):
                 final_reward=float(arrays["final"][g]))
 
 
-def pack_engine(engine):
-    """All slots' records of an mzgo Engine as one uint8 CUDA tensor."""
+def pack_engine(engine, out=None):
+    """All slots' records of an mzgo Engine as one uint8 CUDA tensor (into
+    ``out``, a contiguous uint8 CUDA tensor of exactly the packed size, if
+    given: e.g. one epoch's slice of a staging buffer)."""
     from ._lib import check, lib, ptr, stream_of
     need = ctypes.c_int64()
     check(lib.mzgo_records_pack(engine.handle, None, 0, ctypes.byref(need), stream_of(engine.device)))
-    buf = torch.empty(need.value, dtype=torch.uint8, device=engine.device)
-    check(lib.mzgo_records_pack(engine.handle, ptr(buf), need.value, None, stream_of(engine.device)))
-    return buf
+    if out is None:
+        out = torch.empty(need.value, dtype=torch.uint8, device=engine.device)
+    assert out.dtype == torch.uint8 and out.is_cuda and out.is_contiguous() and out.numel() == need.value
+    check(lib.mzgo_records_pack(engine.handle, ptr(out), need.value, None, stream_of(engine.device)))
+    return out
 
 
 def gather_packed(buf, dst=0, group=None, to_host=True, async_op=False):

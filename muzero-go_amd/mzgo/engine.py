@@ -213,6 +213,25 @@ class Engine:
         self._noise = noise      # keep it alive while moves use it
         check(lib.mzgo_selfplay_inject_noise(self._h, ptr(noise)))
 
+    def record_noise(self, buf):
+        """Test hook: every self-play root's normalised Dirichlet sample into
+        ``buf`` (float64 [G, max_moves, A] on the GPU; None = off)."""
+        if buf is not None:
+            assert buf.dtype == torch.float64 and buf.is_cuda and buf.is_contiguous()
+            assert tuple(buf.shape) == (self.G, self.M, self.A)
+        self._noise_out = buf
+        check(lib.mzgo_selfplay_record_noise(self._h, ptr(buf)))
+
+    def record_nodes(self, buf):
+        """Test hook (tower engines): every node the searches evaluate into
+        ``buf`` (float32 [G, S+1, A+2] on the GPU: logits, reward, value;
+        node 0 the root's logits and value; None = off)."""
+        if buf is not None:
+            assert buf.dtype == torch.float32 and buf.is_cuda and buf.is_contiguous()
+            assert tuple(buf.shape) == (self.G, self.S + 1, self.A + 2)
+        self._nodes_out = buf
+        check(lib.mzgo_tower_record_nodes(self._h, ptr(buf)))
+
     def tower_timing(self, enable):
         """Tower engines: (ms, towers) spent in dynamics towers since the last
         call (synchronises), then timing on/off (mzgo_tower_timing)."""
@@ -222,10 +241,19 @@ class Engine:
         return ms.value, n.value
 
     def counters(self):
-        out = np.zeros(6, np.uint64)
+        out = np.zeros(8, np.uint64)
         check(lib.mzgo_selfplay_counters(self._h, ptr(out), stream_of(self.device)))
         return dict(simulations=int(out[0]), moves=int(out[1]), games_finished=int(out[2]),
-                    playing=int(out[3]), dynamics_convs=int(out[4]), tail_convs=int(out[5]))
+                    playing=int(out[3]), dynamics_convs=int(out[4]), tail_convs=int(out[5]),
+                    prior_rows=int(out[6]), workgroups_started=int(out[7]))
+
+    def wait_started(self, target, stream=None):
+        """Enqueue on ``stream`` (default: the current one) a gate that
+        completes once ``counters()['workgroups_started'] >= target``: a
+        collective queued behind it cannot displace a self-play workgroup of
+        the launch that brings the count there (mzgo_stream_wait_started)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        check(lib.mzgo_stream_wait_started(self._h, int(target), ctypes.c_void_p(s.cuda_stream)))
 
     def record(self, g):
         """Host copy of slot g's game record (numpy arrays)."""

@@ -159,9 +159,9 @@ def test_spawn_ranks_stops_the_others_when_a_rank_fails():
 
 
 def _per_epoch_worker(rank, world, port, out):
-    """Every epoch's packed records gathered asynchronously (bench.py's
-    timed loop), waited on at the end: rank 0 holds each epoch's buffers
-    from every rank, in order."""
+    """Several asynchronous gathers in flight (mzgo.selfplay's per-batch
+    gathers), waited on at the end: rank 0 holds each one's buffers from
+    every rank, in order."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -185,6 +185,42 @@ def test_gather_every_epoch_async_gloo():
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_per_epoch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == [[0, 1], [10, 11], [20, 21]]
+
+
+def _staged_worker(rank, world, port, out):
+    """bench.py's timed loop: every epoch's packed records into its slice of
+    a staging buffer, ONE gather at the end; rank 0 splits each rank's part
+    back into epochs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        steps, per = 3, 64
+        staged = torch.empty(steps * per, dtype=torch.uint8)
+        for epoch in range(steps):
+            staged[epoch * per:(epoch + 1) * per] = 10 * epoch + rank
+        work, parts = mdist.gather_packed(staged, async_op=True)
+        work.wait()
+        if rank == 0:
+            out.put([[int(p[e * per]) for p in parts] for e in range(steps)])
+        else:
+            assert parts is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_staged_epochs_one_gather_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_staged_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

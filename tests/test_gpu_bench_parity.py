@@ -19,9 +19,10 @@ not), so its trees are checked here at those sizes, not only through
   streams and injected Dirichlet sample: identical root-child visit counts,
   root visit count S, root value within 1e-5 (fp32 network).
 
-The sampled-noise run (exactly the bench's code path) is checked for the
-board/record/counter invariants and root visit totals; the injected-noise run
-(same kernel, same sizes; only the Dirichlet source differs) carries the
+The sampled-noise run (exactly the bench's code path) records the Dirichlet
+sample each root drew (test hook ``Engine.record_noise``) and its sampled
+roots are re-searched by the oracle with that sample; the injected-noise run
+(same kernel, same sizes; only the Dirichlet source differs) gets the same
 tree comparison.
 """
 import numpy as np
@@ -60,15 +61,18 @@ def _noise_table(G, M, A):
     return out
 
 
-def _play(net, G, S, check, noise=None):
+def _play(net, G, S, check, noise=None, record=None):
     """One epoch of G games from the empty board; returns the histories and
     the trees (root-child visits, root visits, node count) left by the moves
-    in ``check`` = {move: [games]}."""
+    in ``check`` = {move: [games]}.  record: a float64 [G, M, A] GPU buffer
+    that receives every root's normalised Dirichlet sample (test hook)."""
     import mzgo
     sp = mzgo.SelfPlay(net, G, S, seed=SEED)
     eng = sp.engine
     if noise is not None:
         eng.inject_noise(noise)
+    if record is not None:
+        eng.record_noise(record)
     A = eng.A
     c0 = eng.counters()                    # net.engine() may hand back a used engine
     sp.reset(epoch=0)
@@ -90,6 +94,8 @@ def _play(net, G, S, check, noise=None):
     hists = sp.histories()
     if noise is not None:
         eng.inject_noise(None)
+    if record is not None:
+        eng.record_noise(None)
     return hists, trees, c
 
 
@@ -187,32 +193,44 @@ def test_selfplay_bench_config_matches_oracle(N, G, S, check):
     A, M = N * N + 1, N * N
     net = _net(N)
 
-    # (1) the bench's exact path: sampled Dirichlet noise
-    hists, trees, c = _play(net, G, S, check)
+    onet = OracleNet(deterministic_state_dict(96, A, 0))
+
+    def against_oracle(hists, trees, noise):
+        assert trees, "no sampled root was still playing"
+        for (g, mv), t in sorted(trees.items()):
+            obs = hists[g].observations[mv]
+            hooks = SearchHooks(SEED, g, mv)
+            nz = noise[g, mv]
+            ref = MCTS(onet, A, S, choice=lambda seq, sim, h=hooks: seq[h.choice_index(len(seq), sim)],
+                       noise=lambda p, a, e, nz=nz: (1 - e) * p + e * nz)
+            with torch.no_grad():
+                r_root, _, r_value = ref.run(obs)
+            r_vis = np.array([r_root.children[a]["node"].visit_count if r_root.children[a]["node"] else 0
+                              for a in range(A)])
+            np.testing.assert_array_equal(t["visits"], r_vis, err_msg=f"game {g} move {mv}")
+            assert t["root_n"] == r_root.visit_count == S
+            assert abs(t["value"] - r_value) < 1e-5, (g, mv, t["value"], r_value)
+            assert abs(hists[g].values[mv] - r_value) < 1e-5
+
+    # (1) the bench's exact path: Dirichlet noise sampled on the device; the
+    # sample each root drew is recorded (test hook) and the oracle re-searches
+    # the sampled roots with it
+    drawn = torch.zeros(G, M, A, dtype=torch.float64, device="cuda")
+    hists, trees, c = _play(net, G, S, check, record=drawn)
     _replay_all(hists, N, S, c)
+    drawn = drawn.cpu().numpy()
+    for g, h in enumerate(hists):                  # a Dirichlet sample per move played
+        rows = drawn[g, :len(h)]
+        assert (rows > 0).all() and np.allclose(rows.sum(1), 1.0, atol=1e-12), g
     for (g, mv), t in trees.items():
         assert t["root_n"] == S and int(t["visits"].sum()) == S, (g, mv)
+    against_oracle(hists, trees, drawn)
 
-    # (2) injected noise: the trees against the oracle's MCTS.run
+    # (2) injected noise (the counter-stream uniforms of oracle.rng): the same comparison
     noise = _noise_table(G, M, A)
     hists, trees, c = _play(net, G, S, check, noise=noise)
     _replay_all(hists, N, S, c)
-    assert trees, "no sampled root was still playing"
-    onet = OracleNet(deterministic_state_dict(96, A, 0))
-    for (g, mv), t in sorted(trees.items()):
-        obs = hists[g].observations[mv]
-        hooks = SearchHooks(SEED, g, mv)
-        nz = noise[g, mv]
-        ref = MCTS(onet, A, S, choice=lambda seq, sim, h=hooks: seq[h.choice_index(len(seq), sim)],
-                   noise=lambda p, a, e, nz=nz: (1 - e) * p + e * nz)
-        with torch.no_grad():
-            r_root, _, r_value = ref.run(obs)
-        r_vis = np.array([r_root.children[a]["node"].visit_count if r_root.children[a]["node"] else 0
-                          for a in range(A)])
-        np.testing.assert_array_equal(t["visits"], r_vis, err_msg=f"game {g} move {mv}")
-        assert t["root_n"] == r_root.visit_count == S
-        assert abs(t["value"] - r_value) < 1e-5, (g, mv, t["value"], r_value)
-        assert abs(hists[g].values[mv] - r_value) < 1e-5
+    against_oracle(hists, trees, noise)
 
 
 @pytest.mark.timeout(600)

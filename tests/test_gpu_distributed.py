@@ -60,22 +60,30 @@ def test_selfplay_cli_gpus_flag_starts_the_ranks(tmp_path):
     assert not mismatch and not errors, (mismatch, errors)
 
 
-def test_bench_gpus_2_starts_two_ranks_and_gathers_every_epoch():
+def test_bench_gpus_2_starts_two_ranks_and_gathers_every_epoch_once():
     """``bench.py --gpus 2`` as the driver runs it (no launcher): two rank
-    processes (here both on cuda:0 with gloo standing in for RCCL), one
-    record gather per timed epoch, n_gpus 2 in the rank-0 line."""
+    processes (here both on cuda:0 with gloo standing in for RCCL), every
+    timed epoch's records staged and gathered in one collective at the end
+    of the timed loop, n_gpus 2 in the rank-0 line, the CPU
+    baseline measured by the launcher before the ranks start, and no
+    1-GPU counters or phase shares attached to the 2-GPU line."""
     import json
     env = dict(os.environ, MZGO_SHARE_DEVICE="1", MZGO_DIST_BACKEND="gloo")
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MZGO_CPU_BASELINE"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
-                        "--no-cpu-baseline"], env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+                        "--cpu-budget", "2", "--cpu-procs", "2"], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3
     assert out["config"]["parallelism"] == "game-sharded x2"
-    assert out["gather"]["count"] == 3 and out["gather"]["per_step"] == 1
-    assert out["gather"]["bytes_per_rank"] > 256 * 81 * 82 * 8
+    assert out["gather"]["count"] == 1 and out["gather"]["epochs_per_gather"] == 3
+    assert out["gather"]["bytes_per_epoch_per_rank"] > 256 * 81 * 82 * 8
+    assert out["gather"]["bytes_per_rank"] == 3 * out["gather"]["bytes_per_epoch_per_rank"]
     assert out["value"] > 0
+    cb = out["cpu_baseline"]
+    assert cb["cores"] == 2 and cb["value"] > 0 and cb["measured_in"].startswith("launcher"), cb
+    assert "pmc_source" not in out["roofline"]["units"] and "phases" not in out, out["roofline"]

@@ -393,3 +393,81 @@ def test_tower_chain_wait_expiry_is_reported(monkeypatch):
     sp.reset()
     sp.move()
     assert sp.engine.counters()["moves"] >= G
+
+
+class _ReplayNet:
+    """The device's own per-node tower outputs (Engine.record_nodes) as a
+    network for oracle.mcts.MCTS: a latent is the device node id; expanding
+    (node p, action a) returns the device's child of p at a with the logits,
+    reward and value the tower produced for it.  An expansion the device did
+    not make is a divergence of the searches and fails at once."""
+
+    def __init__(self, nodes, child, A):
+        self.nodes, self.child, self.A = nodes, child, A
+
+    def initial_inference(self, obs):
+        o = self.nodes[0]
+        return (torch.zeros(1, 1, dtype=torch.int64), torch.tensor([[o[self.A + 1]]]),
+                torch.from_numpy(o[:self.A].copy()).reshape(1, self.A))
+
+    def recurrent_inference(self, latent, action):
+        p, a = int(latent.reshape(-1)[0]), int(action.reshape(-1)[0])
+        c = int(self.child[p, a])
+        assert c > 0, f"the oracle expanded (node {p}, action {a}), which the device search did not"
+        o = self.nodes[c]
+        return (torch.tensor([[c]]), torch.tensor([[o[self.A]]]), torch.tensor([[o[self.A + 1]]]),
+                torch.from_numpy(o[:self.A].copy()).reshape(1, self.A))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("moves,seed,S", C5_TREE_CASES, ids=[f"m{m}_s{s}_S{S}" for m, s, S in C5_TREE_CASES])
+def test_tower_config5_tree_exact_replay(moves, seed, S):
+    """Config 5's real network (19x19, C=256, 20 blocks): the oracle's
+    MCTS.run (self_play.py:148-237 restated) driven by the device's OWN tower
+    outputs per node (logits, reward, value as k_texpand / k_troot produced
+    them), the same counter streams and the same injected noise, must build
+    the device's tree exactly: identical root-child visits, every node's
+    visit count and value sum (the same f64 additions in the same order).
+    Any difference is a search defect, not bf16 rounding -- the bounded test
+    above compares against a separately computed (bf16-emulating) network."""
+    import mzgo
+    from oracle.mcts import MCTS as OracleMCTS
+    from oracle.positions import random_position
+    from oracle.rng import SearchHooks, injected_noise
+    N, C, blocks = 19, 256, 20
+    A = N * N + 1
+    net = _nets(N, C, blocks)[0]
+    obs = random_position(N, moves, seed).astype(np.float64)
+    sseed, game, move = 17, 5, moves
+    noise = injected_noise(sseed, game, move, A)
+    m = mzgo.MCTS(net, A, S, seed=sseed, game=game)
+    eng = net.engine(num_games=1, num_simulations=S, **m.cfg)
+    rec = torch.zeros(1, S + 1, A + 2, dtype=torch.float32, device="cuda")
+    eng.record_nodes(rec)
+    try:
+        m.run(obs, move_index=move, noise=torch.from_numpy(noise))
+    finally:
+        eng.record_nodes(None)
+    t = eng.tree(0)
+    nodes = rec[0].cpu().numpy()
+    hooks = SearchHooks(sseed, game, move)
+    om = OracleMCTS(_ReplayNet(nodes, t["child"], A), A, S,
+                    choice=lambda seq, sim: seq[hooks.choice_index(len(seq), sim)],
+                    noise=lambda p, a, e: (1 - e) * p + e * noise)
+    oroot, _, ovalue = om.run(obs)
+    # walk both trees together: node for node, visits and value sums
+    stack, seen = [(oroot, 0)], 0
+    while stack:
+        on, dn = stack.pop()
+        seen += 1
+        assert on.visit_count == int(t["visits"][dn]), (dn, on.visit_count, int(t["visits"][dn]))
+        assert on.value_sum == float(t["value_sum"][dn]), (dn, on.value_sum, float(t["value_sum"][dn]))
+        for a, c in on.children.items():
+            dc = int(t["child"][dn][a])
+            if c["node"] is None:
+                assert dc < 0, (dn, a, dc)
+            else:
+                assert dc > 0, (dn, a)
+                stack.append((c["node"], dc))
+    assert seen == int(t["n"]), (seen, int(t["n"]))
+    assert oroot.visit_count == S
