@@ -21,13 +21,14 @@ on the device, every game of a batch at once) and trains on it:
   (B x 10 recurrent steps, each one launch for all B) and ONE optimizer step
   on their summed gradient; the bootstrap values of every (trajectory, unroll
   step) pair come from one batched ``initial_inference`` on the HIP engine.
-  On the GPU the unroll's forward runs on the HIP kernels
+  With ``hip_forward=True`` the unroll's forward runs on the HIP kernels
   (``initial_inference_hip`` / ``recurrent_inference_hip``: the engine's
   k_initial_inference / k_recurrent_inference for the 3x3 convs, autograd
   Functions whose backward is the HIP kernels of csrc/mzgo_train.hip for every
   3x3 conv -- the dynamics conv from its saved input and output, the
   representation's three after recomputing its two hidden activations on the
-  same kernels); the 1x1 heads stay torch ops on the engine's latents.
+  same kernels); the 1x1 heads stay torch ops on the engine's latents.  The
+  default is torch's ops (MIOpen), measured 8 % faster at main.py's sizes.
 
 ``initial_inference_torch`` / ``recurrent_inference_torch`` restate
 main.py:72-144 with torch ops on the module's own parameters (reference
@@ -376,8 +377,13 @@ class MuZeroTrainer:
         if mode not in ("reference", "batched"):
             raise ValueError(f"mode must be 'reference' or 'batched', not {mode!r}")
         self.net = net
-        # batched mode on the GPU: the unroll's forward on the HIP kernels
-        self.hip_forward = (next(net.parameters()).device.type == "cuda") if hip_forward is None else hip_forward
+        # batched mode: the unroll's forward and 3x3-conv backward on the HIP
+        # kernels (hip_forward=True) or on torch's ops (MIOpen convs, the
+        # default): measured at main.py's 6x6 / C=128 / batch 128 x unroll 10,
+        # the network part takes 10.49 ms on the HIP kernels and 9.71 ms on
+        # MIOpen, the whole step 22.1 vs 21.0 ms (scripts/trainer_timing.py,
+        # profiles/r5_trainer_step.json), so the faster one is the default
+        self.hip_forward = False if hip_forward is None else hip_forward
         self.config = config or TrainConfig()
         self.mode = mode
         self.action_size = net.board_size ** 2 + 1

@@ -47,6 +47,15 @@ out = {
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["hbm_bytes_per_launch"] = 2 * mean["FETCH_SIZE"] * 1024 + mean["WRITE_SIZE"] * 1024
     out["hbm_GBps"] = out["hbm_bytes_per_launch"] / (out["avg_duration_ms"] / 1e3) / 1e9
+    out["hbm_accounting"] = ("2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE doubled on gfx950, "
+                             "calibrated on 16-B/lane streaming reads; an upper bound for narrower reads)")
+    # the same command's memory-side requests by size (scripts/pmc_tcc.sh -> summarize_tcc.py), if run
+    tcc = os.path.join("profiles", f"{tag}_tcc.json")
+    if os.path.exists(tcc):
+        t = json.load(open(tcc))
+        out["hbm_bytes_per_launch_requests_x_size"] = t["hbm_bytes_per_launch"]
+        out["tcc"] = {k: t[k] for k in ("read_requests", "write_requests", "l2_hit_rate")}
+        out["tcc"]["source"] = f"profiles/{tag}_tcc.json"
 c = mean
 dur = out["avg_duration_ms"] / 1e3
 if "GRBM_GUI_ACTIVE" in c:
