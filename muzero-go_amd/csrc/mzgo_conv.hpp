@@ -122,7 +122,7 @@ __device__ __forceinline__ void conv3x3_direct(const float* __restrict__ lds_in,
   static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
   typedef typename WFrag<MGP>::T wfrag;
 
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   const int wave = wave_id();
   const int kq = lane >> 4;       // k row of this lane inside a k-step (B operand)
   const int col = lane & 15;      // cell column of this lane (B operand / accumulator)
@@ -373,7 +373,7 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
   static_assert(NH == 0 || S::NCOG == 2, "head partials assume two cout groups");
   typedef typename WFrag<MGP>::T wfrag;
 
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   const int wave = __builtin_amdgcn_readfirstlane(wave_id());   // scalar: uniform branches
   const int half = wave / 4, wl = wave % 4;                      // k-half, wave within the half
   const int kq = lane >> 4, col = lane & 15;
@@ -413,11 +413,9 @@ __device__ __forceinline__ void conv3x3_ring(const float* lds_in, float* ring, c
 
   if (active) {
     auto issue = [&](int c) {
-#ifndef MZGO_DIAG_NODMA
 #pragma unroll
       for (int p = 0; p < R::NGLDS; ++p)
         dma16(wsrc + (size_t)c * R::SLOT + p * 1024, ring0 + (uint32_t)((c % NSLOT) * R::SLOT + p * 1024));
-#endif
     };
 #pragma unroll
     for (int c = 0; c < NSLOT - 1; ++c)

@@ -125,18 +125,8 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
     f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
     for (int k = 0; k < X::PERL; ++k) {
-#ifdef MZGO_DIAG_XNOE
-      e[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#else
       e[k] = E4[reg * X::C4 + j + X::LPC * k];
-#endif
     }
-#ifdef MZGO_DIAG_XNOY
-    if (L::CACHE && hit) {
-#pragma unroll
-      for (int k = 0; k < X::PERL; ++k) y[k] = f32x4{0.2f, 0.2f, 0.2f, 0.2f};
-    } else
-#endif
     if (L::CACHE && hit) {
 #pragma unroll
       for (int k = 0; k < X::PERL; ++k) y[k] = C4[(size_t)cl * X::C4 + j + X::LPC * k];
@@ -153,11 +143,6 @@ __device__ __forceinline__ void expand_heads(L& lds, const float* __restrict__ Y
     for (int k = 0; k < X::PERL; ++k) {
       const int c4 = j + X::LPC * k;
       f32x4 wr, wv, wp;
-#ifdef MZGO_DIAG_XNOW
-      if (true) {
-        wr = f32x4{0.1f, 0.1f, 0.1f, 0.1f}; wv = wr; wp = wr;
-      } else
-#endif
       if (lw) {
         wr = CW[c4]; wv = CW[X::C4 + c4]; wp = CW[2 * X::C4 + c4];
       } else {
@@ -243,13 +228,8 @@ struct ExpandPlan {
 // orders xw for the wave's readers (wave_lds_sync).
 // POL = false (lazy policy head, batched children): the totals only; the
 // policy sums are formed if a select ever reaches the child (policy_sums_wg).
-// GLOBAL_Y boards: Y loads one pass pair ahead (MZGO_NO_EXPAND_PREFETCH for
-// the A/B build without; the same values either way)
-#ifdef MZGO_NO_EXPAND_PREFETCH
-constexpr bool kExpandPrefetch = false;
-#else
-constexpr bool kExpandPrefetch = true;
-#endif
+// GLOBAL_Y boards: Y loads one pass ahead (+0.5 % at 19x19 in the same call
+// against none, round 4)
 template <class G, int PROW, bool POL = true>
 __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const float* ew, const float* hw,
                                             const ExpandPlan<G>& plan, float& rsum, float& vsum) {
@@ -300,11 +280,7 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
     f32x4 y[X::PERL], e[X::PERL];
 #pragma unroll
     for (int k = 0; k < X::PERL; ++k) {
-#ifdef MZGO_DIAG_YL1
-      y[k] = Y4[(p & 1) * 8 * X::C4 + 8 * k];          // (diagnostic: 16 cells, L1-resident)
-#else
       y[k] = Y4[p * 8 * X::C4 + 8 * k];
-#endif
       e[k] = E4[8 * k];
     }
     const bool live = G::CELLS % 8 == 0 || !last || cg + 8 * p < G::CELLS;
@@ -327,7 +303,7 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
     // every pass unrolled, offsets from the plan's registers
 #pragma unroll
     for (int p = 0; p < P; ++p) pass(p, (plan.off[p >> 1] >> (16 * (p & 1))) & 0xFFFFu, p == P - 1);
-  } else if constexpr (kExpandPrefetch) {
+  } else {
     // pass pairs, one LDS table read per pair (19x19: 23 pairs), Y streamed
     // from L2 one pass ahead: pass p + 1's loads are in flight while pass p
     // is computed (each wave's passes are latency-bound on L2)
@@ -346,19 +322,6 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
       if (pp + 1 < P / 2) ldy(2 * pp + 2, ya);
       pass_y(2 * pp + 1, yb, w2 >> 16, pp + 1 == P / 2);
     }
-  } else {
-    // pass pairs, one LDS table read per pair (19x19: 23 pairs); the last
-    // pair (whose second pass holds the board's last cells) peeled off
-    static_assert(P % 2 == 0, "whole pass pairs");
-#pragma unroll 1
-    for (int pp = 0; pp < P / 2 - 1; ++pp) {
-      const uint32_t w2 = plan.pair(pp, cg);
-      pass(2 * pp, w2 & 0xFFFFu, false);
-      pass(2 * pp + 1, w2 >> 16, false);
-    }
-    const uint32_t w2 = plan.pair(P / 2 - 1, cg);
-    pass(P - 2, w2 & 0xFFFFu, false);
-    pass(P - 1, w2 >> 16, true);
   }
   f32x2 dr2 = {0.f, 0.f}, dv2 = {0.f, 0.f};
 #pragma unroll

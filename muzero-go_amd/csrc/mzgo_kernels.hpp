@@ -49,6 +49,24 @@ __device__ __forceinline__ T* launder_global(T* p) {
   asm volatile("" : "+s"(x));
   return (T*)reinterpret_cast<__attribute__((address_space(1))) T*>(x);
 }
+// The search's f64 parameters made opaque per move as well: the constants
+// derived from them (the Gamma sampler's d and 1 / sqrt(9 d), f32 1 - eps)
+// are then formed per move instead of being hoisted to the kernel entry and
+// kept (spilled, k_selfplay_move<19,96>) across the whole game
+__device__ __forceinline__ double launder_f64(double v) {
+  unsigned long long x = (unsigned long long)__double_as_longlong(v);
+  asm volatile("" : "+s"(x));
+  return __longlong_as_double((long long)x);
+}
+__device__ __forceinline__ SearchParams launder_search(const SearchParams& p) {
+  SearchParams r = p;
+  r.c_puct = launder_f64(p.c_puct);
+  r.discount = launder_f64(p.discount);
+  r.dirichlet_alpha = launder_f64(p.dirichlet_alpha);
+  r.dirichlet_epsilon = launder_f64(p.dirichlet_epsilon);
+  r.pass_epsilon = launder_f64(p.pass_epsilon);
+  return r;
+}
 __device__ __forceinline__ NetParams launder_params(const NetParams& n) {
   NetParams r;
 #define MZGO_L(f) r.f = launder_global(n.f);
@@ -1065,7 +1083,7 @@ __device__ __forceinline__ int root_batch(Smem<G>& sm, const NetParams& np, cons
         const int a = lane_id_local() + 64 * j;
         n += __popcll(__ballot(a < G::A && T.root_prior(a) > 0.0));
       }
-      if (lane_id() == 0) sm.t.bcast = n < S ? n : S;
+      if (lane_id_local() == 0) sm.t.bcast = n < S ? n : S;
     }
     __syncthreads();
     const int K = sm.t.bcast;
@@ -1175,43 +1193,18 @@ struct VerifyLds {
 // is checked in groups of this many levels): 8 at 9x9 and below, 2 at 19x19
 template <class G>
 constexpr int verify_depth() { return G::AP > 2 ? 2 : 8; }
-// leaves deeper than this replay their batch one select at a time instead
-// (MZGO_VERIFY_MAX_DEPTH to compare the two; the trees are the same)
-#ifndef MZGO_PICK_ALL
-#define MZGO_PICK_ALL 1   // unshared batches: picks one by one, streamed (0) or all at once (1; round 3: +0.6 %)
-#endif
-#ifdef MZGO_VERIFY_MAX_DEPTH
-constexpr int kVerifyMaxDepth = MZGO_VERIFY_MAX_DEPTH;
-#else
-constexpr int kVerifyMaxDepth = 1 << 20;
-#endif
-// batches of fewer children replay one select at a time (unshared batches;
-// the trees are the same either way).  Sweep of the minimum (9x9 / 256 / 200
-// epoch, same call): 2 (every batch in parallel) 75.6 M sims/s, 3 75.1,
-// 4 76.1, 6 77.1, 8 77.0, 12 74.1, 16 70.2, never 38.3
-#ifndef MZGO_VERIFY_MIN_B
-#define MZGO_VERIFY_MIN_B 6
-#endif
-constexpr int kVerifyMinB = MZGO_VERIFY_MIN_B;
-// default rule: sequential while (B - 1) * (depth + 1) < 16 (same call: the
-// minimum-B rule at 6 77.0-77.2 M sims/s; K = 8 / 12 / 16 / 24: 77.1 / 78.1 /
-// 79.0 / 77.8; a second call, K = 14 / 16 / 18 / 20: 78.5 / 78.8 / 78.6 / 78.5)
-#ifndef MZGO_VERIFY_SEQ_K
-#define MZGO_VERIFY_SEQ_K 16
-#endif
-// (B - 1) * (depth + 1) < K: the batch's B - 1 replayed selects (a walk of
-// depth + 1 levels each) against the parallel replay's fixed cost
-__device__ __forceinline__ bool replay_sequential(int B, int depth) {
-  if constexpr (MZGO_VERIFY_SEQ_K > 0) return (B - 1) * (depth + 1) < MZGO_VERIFY_SEQ_K;
-  else return B < kVerifyMinB;
-}
-// HBM trees with helper workgroups (shared jobs): the same rule with its own K
-// (0: always the shared parallel replay; 32: profiles/r4x_shared_seq_ab.txt)
-#ifndef MZGO_SHARED_SEQ_K
-#define MZGO_SHARED_SEQ_K 32
-#endif
+// A speculative batch of B children of a leaf at depth D is replayed one
+// select at a time (B - 1 walks of D + 1 levels) while (B - 1) * (D + 1) <
+// kSeqK, else by the parallel replay (verify_batch; the trees are the same
+// either way).  Measured, 9x9 / 256 / 200 epoch, same call: K = 8 / 12 / 16 /
+// 24: 77.1 / 78.1 / 79.0 / 77.8 M sims/s (a minimum-B rule at its best, 6:
+// 77.0-77.2); HBM trees with helper workgroups (shared jobs, 19x19): K = 0 /
+// 8 / 16 / 32 / 64: 37.8 / 37.8 / 38.0 / 38.3 / 37.7 M
+// (profiles/r4x_shared_seq_ab.txt)
+constexpr int kSeqK = 16, kSharedSeqK = 32;
+__device__ __forceinline__ bool replay_sequential(int B, int depth) { return (B - 1) * (depth + 1) < kSeqK; }
 __device__ __forceinline__ bool replay_parallel(bool shared, int B, int depth) {
-  if (shared) return !(MZGO_SHARED_SEQ_K > 0 && (B - 1) * (depth + 1) < MZGO_SHARED_SEQ_K);
+  if (shared) return (B - 1) * (depth + 1) >= kSharedSeqK;
   return !replay_sequential(B, depth);
 }
 
@@ -1612,10 +1605,6 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     const int* info = J.info();
     const int B = info[0], nid0 = info[1], leaf = info[2], net = info[3], kind = info[4];
     const NetParams np = select_params(net != 0, np_b, np_a);
-#ifdef MZGO_DIAG_HELPER_SKIP
-    // (diagnostic builds: helpers leave job kinds in the bit mask to the game's workgroup)
-    if ((MZGO_DIAG_HELPER_SKIP >> kind) & 1) continue;
-#endif
     if (kind == 3) {                                   // replay checks of a batch (verify_batch)
       constexpr int DV = verify_depth<G>();
       typedef VerifyLds<G, DV> V;
@@ -1778,7 +1767,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     if (!pending) {
       if (wave_id() == 0) {
         const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st);
-        if (lane_id() == 0) sm.t.action = a;
+        if (lane_id_local() == 0) sm.t.action = a;
         st.wave_add(92, 1);
         st.wave_add(95, (unsigned long long)sm.t.depth);
       }
@@ -1797,7 +1786,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       __syncthreads();
       if (wave_id() == 0) {
         const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st, xn, xd);
-        if (lane_id() == 0) sm.t.action = a;
+        if (lane_id_local() == 0) sm.t.action = a;
       }
       __syncthreads();
     }
@@ -1921,20 +1910,16 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         if (shared_jobs<G>(sp)) {
           batch_expand_shared<G, Acc::LDS>(sm, np, sp, E, g, TV, B, nid, leaf, sp.net, yleaf, um, nun - 1, 1, key,
                                            sim + 1, &st, prepicked, [&]() {
-                                             if (depth <= kVerifyMaxDepth && replay_parallel(true, B, depth))
+                                             if (replay_parallel(true, B, depth))
                                                verify_preload<G, Acc>(sm, sp, TV, T, nact, depth);
                                            });
           st.lap(71);
         } else {
           if (wave_id() == 0) {
-#if MZGO_PICK_ALL
             // every pick at once (pick_all), then published together
             pick_all<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &st);
             wave_lds_sync();
-            if (lane_id() == 0) __hip_atomic_store(&sm.t.npick, B, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-            pick_sequence<G>(um, nun - 1, 1, B - 1, key, sim + 1, sm.u.f.acts, &sm.t.npick, G::WAVES - 1, &st);
-#endif
+            if (lane_id_local() == 0) __hip_atomic_store(&sm.t.npick, B, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             st.lap(71);
           }
           batch_expand<G, Acc::LDS>(sm, np, sp, TV, B, nid, yleaf, &st);
@@ -1942,7 +1927,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         __syncthreads();
         st.lap(5);
         if (!(Acc::LDS || shared_jobs<G>(sp))) rows += B;
-        if (depth <= kVerifyMaxDepth && replay_parallel(shared_jobs<G>(sp), B, depth)) {
+        if (replay_parallel(shared_jobs<G>(sp), B, depth)) {
           const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st, shared_jobs<G>(sp));
           nodes += m;
           sim += m;
@@ -2023,7 +2008,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     if (wave_id() == 1) {
       const unsigned long long t1 = st.now();
       int* crow = TV.child + (size_t)nid * G::A;        // the new node: no children yet
-      for (int i = lane_id(); i < G::A; i += 64) crow[i] = -1;   // (before its priors are published)
+      for (int i = lane_id_local(); i < G::A; i += 64) crow[i] = -1;   // (before its priors are published)
       float x[G::AP];
       if (factored) logits_regs<G, 1>(heads, true, sm.t.hsc, x);
       else logits_regs<G, Smem<G>::HEAD_PARTS>(heads, true, sm.t.hsc, x);
@@ -2036,8 +2021,8 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
       float r, v;
       if (factored) heads_value<G, 1>(heads, true, sm.t.hsc, r, v);
       else heads_value<G, Smem<G>::HEAD_PARTS>(heads, true, sm.t.hsc, r, v);
-      if (lane_id() == (a & 63)) T.set_child(leaf, a, nid);
-      if (lane_id() == 0) nact[nid] = a;
+      if (lane_id_local() == (a & 63)) T.set_child(leaf, a, nid);
+      if (lane_id_local() == 0) nact[nid] = a;
       backup<G>(T, depth, nid, (double)r + sp.discount * (double)v, sp.variant == 0);
     }
     st.lap(3);
@@ -2328,7 +2313,7 @@ __device__ __forceinline__ int choose_action_main(TreeLds<G>& t, const TreeView&
 template <class G>
 __device__ __forceinline__ int choose_action(TreeLds<G>& t, const TreeView& T, int compat, double temperature,
                                     uint64_t key, double* pol) {
-  const int lane = lane_id();
+  const int lane = lane_id_local();
   // visit_counts * valid_mask (zeros under compat "reference", §0.6)
   for (int a = lane; a < G::A; a += 64) {
     double vc = 0.0;
@@ -2505,11 +2490,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   // pp.moves moves of this game in one launch (the board stays in LDS between
   // them): a game's moves run back to back on its CU instead of every move of
   // every game waiting for the slowest game's move at a launch boundary
-#ifdef MZGO_ONE_MOVE
-  for (int step = 0; step < 1; ++step) {             // (experiment: the loop's register cost)
-#else
   for (int step = 0; step < pp.moves; ++step) {
-#endif
 #ifdef MZGO_STAMPS
   unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   tm[0] = __builtin_amdgcn_s_memtime();
@@ -2541,7 +2522,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #ifdef MZGO_STAMPS
   tm[1] = __builtin_amdgcn_s_memtime();
 #endif
-  SearchParams spm = sp;
+  SearchParams spm = launder_search(sp);
   spm.net = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? 1 : 0;
   run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
                 tm ? tm + 2 : nullptr, noise_out);
@@ -2554,7 +2535,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     const double temp = mv < pp.temperature_moves ? pp.temperature : 0.0;
     const int a = sp.variant == 1 ? choose_action_main<G>(sm.t, T, key, E.rec_policy + rec * G::A)
                                   : choose_action<G>(sm.t, T, sp.compat, temp, key, E.rec_policy + rec * G::A);
-    if (lane_id() == 0) {
+    if (lane_id_local() == 0) {
       sm.bc[0] = a;
       E.rec_action[rec] = a;
       const int n = T.visits[0];

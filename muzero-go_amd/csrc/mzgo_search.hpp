@@ -359,7 +359,7 @@ __device__ __forceinline__ void finalize_heads(const float* hp, bool has_reward,
   float r, v;
   heads_value<G, NPART>(hp, has_reward, hsc, r, v);
   heads_logits<G, NPART>(hp, has_reward, hsc, logits);
-  if (lane_id() == 0) { *value = v; *reward = r; }
+  if (lane_id_local() == 0) { *value = v; *reward = r; }
 }
 
 // Child priors of a new node (self_play.py:204-224) from its logits x (a =

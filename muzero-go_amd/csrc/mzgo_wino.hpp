@@ -27,30 +27,9 @@
 #pragma once
 #include "mzgo_common.hpp"
 
-#ifndef MZGO_WINO_SYNC
-#define MZGO_WINO_SYNC 0
-#endif
-#ifndef MZGO_WINO_PF
-#define MZGO_WINO_PF 8
-#endif
-#ifndef MZGO_NT_STORE
-#define MZGO_NT_STORE 1   // whole-row streaming stores of node latents
-#endif
-#ifndef MZGO_WINO_PINB
-#define MZGO_WINO_PINB 1
-#endif
-#ifndef MZGO_WINO_PRIO
-#define MZGO_WINO_PRIO 1
-#endif
-#ifndef MZGO_WINO_PK
-#define MZGO_WINO_PK 1
-#endif
-#ifndef MZGO_WINO_XG
-#define MZGO_WINO_XG 2
-#endif
 
 namespace mzgo {
-constexpr int kWinoXG = MZGO_WINO_XG;   // xi per accumulation group (A stream order, pack_wino)
+constexpr int kWinoXG = 2;   // xi per accumulation group (A stream order, pack_wino)
 }
 
 namespace mzgo {
@@ -140,7 +119,6 @@ __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const
     for (int b = 0; b < 5; ++b) d[a][b] = s[a * PW + b];
   float* vb = V + (size_t)quad * 64 + t * 4 + e;         // quad index == (h*S4 + s4)*4 + kq
   constexpr int XSTRIDE = 2 * S4 * 4 * 64;    // floats between xi planes
-#if MZGO_WINO_PK
   // rows in pairs (0,1), (2,3) as packed f32x2 (v_pk_add/v_pk_fma: two rows
   // per instruction); the factor-2 FMAs round exactly like mul + add
   f32x2 u[2][5];
@@ -166,25 +144,6 @@ __device__ __forceinline__ void wino_transform_quad(float* __restrict__ V, const
       vb[((2 * i + 1) * 5 + j) * XSTRIDE] = v[j].y;
     }
   }
-#else
-  float u[4][5];
-#pragma unroll
-  for (int b = 0; b < 5; ++b) {               // BT2 along rows
-    u[0][b] = d[0][b] - d[2][b];
-    u[1][b] = d[1][b] + d[2][b];
-    u[2][b] = d[2][b] - d[1][b];
-    u[3][b] = d[3][b] - d[1][b];
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {               // BT3 along columns
-    const float* q = u[i];
-    vb[(i * 5 + 0) * XSTRIDE] = ((2.f * q[0] + q[1]) - 2.f * q[2]) - q[3];
-    vb[(i * 5 + 1) * XSTRIDE] = (2.f * q[1] + 3.f * q[2]) + q[3];
-    vb[(i * 5 + 2) * XSTRIDE] = (q[2] - 2.f * q[1]) + q[3];
-    vb[(i * 5 + 3) * XSTRIDE] = q[1] - q[3];
-    vb[(i * 5 + 4) * XSTRIDE] = ((2.f * q[3] - 2.f * q[1]) - q[2]) + q[4];
-  }
-#endif
 }
 
 // The halo columns of every raw plane must be 0 before the first wino_input
@@ -442,7 +401,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   constexpr int XH = XI / 2;                  // xi per wave (two xi halves)
   constexpr int KP = CIN / 16;                // float4 k-positions per xi (4 k-steps each)
   constexpr int L = XH * KP;                  // float4 A loads (and B reads) per wave
-  constexpr int PF = MZGO_WINO_PF;             // A prefetch depth (float4 registers)
+  constexpr int PF = 8;             // A prefetch depth (float4 registers)
   static_assert(2 * MT <= G::WAVES, "one wave per (cout tile, xi half)");
   constexpr int XG = kWinoXG;
   static_assert(XH % XG == 0, "xi groups");
@@ -475,13 +434,6 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(q, 0)];
 #pragma unroll
     for (int g = 0; g < XH / XG; ++g) {       // XG independent accumulation chains
-#if MZGO_WINO_SYNC > 0
-      // pacing barrier: keeps the SIMD's waves in step (oldest-first issue
-      // otherwise leaves the youngest wave to finish alone)
-      if constexpr (2 * MT == G::WAVES)
-        if (g > 0 && g % MZGO_WINO_SYNC == 0) __builtin_amdgcn_s_barrier();
-#endif
-#if MZGO_WINO_PRIO == 1
       // progress-ordered issue: a wave that is ahead drops its priority, so
       // the SIMD's three waves advance together (oldest-first issue otherwise
       // leaves the youngest wave's two MFMA chains to finish alone)
@@ -489,26 +441,6 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       else if (g == 1) __builtin_amdgcn_s_setprio(2);
       else if (g == 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
-#elif MZGO_WINO_PRIO == 2
-      // static priority by age: the younger waves of a SIMD (4-7, 8-11: the
-      // arbitration losers) ahead of the older ones, for the whole GEMM
-      if (g == 0) {
-        if (wave >= 8) __builtin_amdgcn_s_setprio(2);
-        else if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-      }
-#elif MZGO_WINO_PRIO == 3
-      // progress-ordered over all five groups, ties broken for the younger waves
-      if (g == 0) __builtin_amdgcn_s_setprio(3);
-      else if (g == 2) {
-        if (wave >= 4) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(1);
-      } else if (g == 3) {
-        if (wave >= 8) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      } else if (g == 4) {
-        __builtin_amdgcn_s_setprio(0);
-      }
-#endif
       f32x4 acc[XG];
 #pragma unroll
       for (int q = 0; q < XG; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -518,7 +450,6 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         f32x4 a[XG], b[XG];
 #pragma unroll
         for (int q = 0; q < XG; ++q) { a[q] = ar[(pos0 + q) % PF]; b[q] = bn[q]; }
-#ifndef MZGO_DIAG_NOB
         // next B operands
         if (k + 1 < KP) {
 #pragma unroll
@@ -527,24 +458,15 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
 #pragma unroll
           for (int q = 0; q < XG; ++q) bn[q] = bp[bidx((g + 1) * XG + q, 0)];
         }
-#endif
-#if MZGO_WINO_PINB
         __builtin_amdgcn_sched_barrier(0);      // issue the next B reads before these MFMAs
-#endif
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
           for (int q = 0; q < XG; ++q)
             acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][e], b[q][e], acc[q], 0, 0, 0);
-#ifndef MZGO_DIAG_NOA
 #pragma unroll
         for (int q = 0; q < XG; ++q)
-#ifdef MZGO_DIAG_L1A
-          if (pos0 + q + PF < L) ar[(pos0 + q) % PF] = ap[((pos0 + q + PF) % 2) * 64];   // L1-resident (wrong values)
-#else
           if (pos0 + q + PF < L) ar[(pos0 + q) % PF] = ap[(pos0 + q + PF) * 64];
-#endif
-#endif
         // keep the refill loads here: left alone, the scheduler sinks them
         // next to their use (to save VGPRs) and exposes the L2 latency
         __builtin_amdgcn_sched_barrier(0);
@@ -577,9 +499,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
       else { yp[ox] = z0; yp[3 + ox] = z1 - z0; }
     }
   }
-#if MZGO_WINO_PRIO
   __builtin_amdgcn_s_setprio(0);
-#endif
   if (st) { st->wave_add(8 + wave, __builtin_amdgcn_s_memtime() - t_loop); st->lap(6); }
 
   // epilogue constants (the bias was loaded before the GEMM, its latency
@@ -727,11 +647,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         const int co = i / Q, q = i - co * Q;
         const f32x4 v = *reinterpret_cast<const f32x4*>(outs + co * OS + q * 4);
         f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)co * G::CS + c0) + q;
-#if MZGO_NT_STORE
         __builtin_nontemporal_store(v, dst);
-#else
-        *dst = v;
-#endif
       }
     } else {
       const int n = min(c0 + W::SCELLS, out_cells) - c0;

@@ -92,7 +92,12 @@ def _load():
             f"{LIB_PATH} is missing: build the HIP engine first "
             "(python -c 'import __graft_entry__ as g; g.build()' from the repo root)")
     lib = ctypes.CDLL(LIB_PATH)
+    # (an older library loaded for an A/B, MZGO_LIB, may lack newer entry
+    # points: they stay unbound there; the product library has every one)
+    tolerant = "MZGO_LIB" in os.environ
     for name, (res, args) in SIGNATURES.items():
+        if tolerant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
