@@ -247,7 +247,7 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no spar
 
 
 def tower_roofline(N, C, blocks, G, sims, tower_ms, towers, towers_run):
-    """Config 5's dominant kernel: k_tconv (one 3x3 conv of every active
+    """Config 5's dominant kernel: the tower conv (one 3x3 conv of every active
     leaf, bf16 MFMA).  Algorithmic FLOPs per launch = boards x 2 x N^2 x 9 x C^2
     (the conv as the network defines it; the kernel also multiplies the
     16-row tiles' pad rows: executed = boards x 2 x 16*ceil(N^2/16) x 9 x C^2),
@@ -261,7 +261,7 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, towers, towers_run):
     ach = alg / avg_launch_s / 1e12
     # one k_tconv_chain launch per tower (all L convs) unless MZGO_TCONV_CHAIN=0
     chain = os.environ.get("MZGO_TCONV_CHAIN") != "0" and G * (C // 64) <= 256
-    kname = "k_tconv_chain" if chain else ("k_tconv" if os.environ.get("MZGO_TCONV_KS") == "0" else "k_tconv_ks")
+    kname = "k_tconv_chain" if chain else "k_tconv_ks"
     out = {"bound": "mfma", "kernel": f"{kname}<{N}>", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS,
            "unit": "TFLOP/s", "frac": ach / PEAK_BF16_MFMA_TFLOPS, "traffic": None,
            "avg_launch_ms": avg_launch_s * 1e3, "launches_per_simulation": L, "boards_per_launch": boards,
@@ -335,7 +335,7 @@ def tower_main(args, world, rank, local, cpu_ref):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sp.move()
+        sp.move(args.moves_per_step)
     if world > 1:
         from mzgo import distributed as mdist
         mdist.gather_packed(mdist.pack_engine(eng), to_host=False)
@@ -356,9 +356,10 @@ def tower_main(args, world, rank, local, cpu_ref):
         dt, sims, moves = tmax[0].item(), t[1].item(), t[2].item()
     if rank == 0:
         workload = f"{N}x{N} Go self-play, {B}-block residual nets (C={C}), {G} parallel games/GPU, {S} sims/move"
-        roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers, S * args.steps)
+        mps = args.moves_per_step
+        roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers, S * args.steps * mps)
         # the conv kernel's share of the step: launches x average launch / wall time
-        roof["share_of_step"] = roof["avg_launch_ms"] / 1e3 * (2 * B + 1) * S * args.steps / dt
+        roof["share_of_step"] = roof["avg_launch_ms"] / 1e3 * (2 * B + 1) * S * args.steps * mps / dt
         out = {
             "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {B}-block residual "
                       f"nets, {S} sims/move (BASELINE config 5)",
@@ -367,9 +368,11 @@ def tower_main(args, world, rank, local, cpu_ref):
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (deterministic random-init weights, self-play from empty boards)",
             "moves_per_s": moves / dt,
-            "config": {"workload": workload, "step": f"one move of {G} games/GPU ({S} simulations each; "
+            "config": {"workload": workload, "step": (f"{mps} consecutive moves" if mps > 1 else "one move")
+                                                     + f" of {G} games/GPU ({S} simulations each; "
                                                      f"{2 * B + 1} convs per simulation)"
                                                      + (f", from move {args.start_move}" if args.start_move else ""),
+                       "moves_per_step": mps,
                        "board_size": N, "latent_dim": C, "res_blocks": B, "games_per_gpu": G,
                        "sims_per_move": S, "parallelism": f"game-sharded x{world}", "compat": "reference",
                        "precision": "bf16 MFMA operands, fp32 accumulation, bf16 activations",
@@ -506,6 +509,8 @@ def main():
                     help="2: 9x9 / 256 games / 200 sims (the headline, BASELINE configs[1]); "
                          "5: 19x19 / 20-block residual nets / 1600 sims / 64 games (BASELINE configs[4])")
     ap.add_argument("--blocks", type=int, default=20, help="residual blocks (config 5)")
+    ap.add_argument("--moves-per-step", type=int, default=1,
+                    help="config 5: a step = this many consecutive moves of every game (a game segment)")
     ap.add_argument("--start-move", type=int, default=0,
                     help="config 5: time moves from this move on (every game fast-forwarded there first by "
                          "untimed self-play at 8 simulations per move)")

@@ -50,7 +50,7 @@ struct TGeo {
   static constexpr int THREADS = 64, WAVES = 1, TREE_CAP = 0;
 };
 
-// k_tconv geometry for NW waves per workgroup (one workgroup per CU).  The
+// Tower-conv geometry for NW waves per workgroup (one workgroup per CU).  The
 // k-loop runs in steps of one kernel row (3 taps x one 64-channel cin chunk):
 // a step's weight tile is 3 x 64 x 64 bf16 = 24 KiB.
 template <int N, int NW>
@@ -63,12 +63,6 @@ struct TConvGeo {
   static constexpr int WSLOT = 3 * 64 * 64 * 2;         // one step's weight tile
   static constexpr int WPW = WSLOT / 1024 / NW;         // its 1-KiB pieces per wave
   static constexpr int MT = (G::TT + NW - 1) / NW;      // 16-pixel tiles per wave
-  // A-fragment prefetch distance in (tap, tile) groups (MZGO_TCONV_ADIST to experiment)
-#ifdef MZGO_TCONV_ADIST
-  static constexpr int ADIST = MZGO_TCONV_ADIST;
-#else
-  static constexpr int ADIST = 2;
-#endif
   // + bias and head weights (1 KiB) + the landing area of L2 touches (256 B)
   static constexpr int LDS = 2 * PB + 2 * WSLOT + 4 * 64 * 4 + 256;
   static_assert(WPW * NW * 1024 == WSLOT, "whole weight pieces per wave");
@@ -83,50 +77,18 @@ struct TConvGeo {
   }
 };
 
-// GEMM row m -> board cell (raster index), -1 for a pad row.  N >= 16: the
-// first 16 cells of every board row are rows 16y..16y+15 (a tile = 16
-// consecutive pixels of one board row: its A-fragment reads are bank-conflict
-// free, see frag_ld), the remaining columns follow column by column; smaller
-// boards in raster order.
-#ifndef MZGO_TOWER_ROWSEG
-#define MZGO_TOWER_ROWSEG 0
-#endif
-constexpr bool kTowerRowSegments = MZGO_TOWER_ROWSEG != 0;
+// GEMM row m -> board cell (raster order), -1 for a pad row.  (Tiles of 16
+// pixels of one board row, with the conflict-free swizzle below, took the
+// fragment reads' LDS bank conflicts from 0.326 to 0.064 of the LDS cycles
+// and made the conv no faster, round 4: removed in round 5.)
 template <int N>
-__device__ __forceinline__ int tcell(int m) {
-  if constexpr (N >= 16 && kTowerRowSegments) {
-    if (m < 16 * N) return (m >> 4) * N + (m & 15);
-    const int r = m - 16 * N;
-    return r < N * (N - 16) ? (r % N) * N + 16 + r / N : -1;
-  } else {
-    return m < N * N ? m : -1;
-  }
-}
+__device__ __forceinline__ int tcell(int m) { return m < N * N ? m : -1; }
 
 // The position of 16-byte piece j of padded pixel q's 128-byte row is
-// j ^ tswz(q).  A ds_read_b128 serves a wave in 4 lane groups of 16
-// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same +32: one LDS cycle
-// each when its 16 reads hit 16 distinct 16-byte bank slots); a group holds
-// MFMA rows 0-3 and 12-15 of one k piece and rows 4-11 of its neighbour
-// piece.  The slot of (q, j) is 8 (q & 1) + (j ^ tswz(q)), and with tswz(q)
-// = 2 ((q >> 1) & 3) any 16 consecutive pixels fill the 16 slots for every
-// piece pair (the even and the odd pixels each cover the 4 values of
-// (q >> 1) & 3 once in the rows the group reads at piece j and once at
-// j ^ 1, where the XOR moves them to the odd slot values).  Tiles of 16
-// pixels of one board row (kTowerRowSegments) are consecutive for every tap;
-// simulated over the 19x19 conv's fragment reads: 1.13 LDS cycles per lane
-// group (the 3-column tail tiles step by W), against 1.89 for (q >> 1) & 7
-// on raster tiles.  Measured (MZGO_TOWER_SWZ=1 MZGO_TOWER_ROWSEG=1, config
-// 5, rocprofv3): SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.326 -> 0.064,
-// LDS-array cycles -28 %, and k_tconv_ks no faster (25.8-26.0 vs 25.7 us,
-// same call): the fragment reads' conflicts are off the critical path.  The
-// default stays (q >> 1) & 7 on raster tiles, the faster of the two.
-#ifndef MZGO_TOWER_SWZ
-#define MZGO_TOWER_SWZ 0
-#endif
+// j ^ tswz(q): 16 consecutive pixel rows then read their MFMA fragments with
+// few bank conflicts (a chunk's LDS image is still a straight LDS-DMA copy).
 __device__ __forceinline__ int tswz(int q) {
-  if constexpr (MZGO_TOWER_SWZ != 0) return ((q >> 1) & 3) << 1;
-  else return (q >> 1) & 7;
+  return (q >> 1) & 7;
 }
 // element offset of (padded pixel q, channel c) inside one 64-channel chunk
 __device__ __forceinline__ int tpix(int q, int piece) { return q * 64 + ((piece ^ tswz(q)) << 3); }
@@ -177,337 +139,6 @@ __device__ __forceinline__ bf16x8 frag_ld(const char* p) { return *reinterpret_c
 #define STAMP_T(v) do {} while (0)
 #endif
 
-template <int N, int NW>
-__global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
-  typedef TGeo<N> G;
-  typedef TConvGeo<N, NW> T;
-  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
-  STAMP_T(tstart);
-#ifdef MZGO_TCONV_STAMPS
-  unsigned long long acc_wait = 0, acc_bar = 0, acc_mfma = 0;
-  const unsigned long long rstart = __builtin_amdgcn_s_memrealtime();
-#endif
-  const int CO = a.co_chunks, CC = a.ci_chunks;
-  // block -> (board, cout chunk); a board's chunks on one XCD (blocks b, b+8,
-  // ... share one under round-robin dispatch: speed only) when the grid allows
-  const int bid = blockIdx.x;
-  int b, cg;
-  if (a.nboards % 8 == 0) {
-    const int x = bid & 7, k = bid >> 3;
-    b = x + 8 * (k / CO);
-    cg = k % CO;
-  } else {
-    b = bid / CO;
-    cg = bid % CO;
-  }
-  if (a.active && !a.active[b]) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* const patch0 = lds;
-  char* const wring = lds + 2 * T::PB;
-  float* const sbias = reinterpret_cast<float*>(lds + 2 * T::PB + 2 * T::WSLOT);
-  float* const shw = sbias + 64;
-  const bf16* in = a.in + (long long)(a.in_idx ? a.in_idx[b] : b) * a.in_stride;
-  const bf16* wsrc = a.w + (size_t)cg * CC * 9 * 64 * 64;
-  if (tid < 64) {
-    sbias[tid] = a.bias[cg * 64 + tid];
-    if (a.headw)
-      for (int h = 0; h < 3; ++h) shw[h * 64 + tid] = a.headw[h * CO * 64 + cg * 64 + tid];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA counts below start from zero
-
-  // DMA issue helpers (16 B per lane; the LDS destination is base + lane*16).
-  // Step s = 3*cc + ky: weight tile W(s) = taps 3ky..3ky+2 of cin chunk cc,
-  // ring slot s % 2.  After step s's barrier every wave issues its pieces of
-  // W(s+1) and, at ky = 0 and 1, of the next chunk's patch (other buffer);
-  // before step s it waits for W(s): the only DMAs younger than W(s) are the
-  // patch pieces of step s-1.  A chunk's patch is issued at steps ky 0 and 1
-  // of the previous chunk, before W(its first step): the same wait covers it.
-  auto issue_patch_pieces = [&](int cc, int buf, int k0, int k1) {
-    const char* src = reinterpret_cast<const char*>(in + (size_t)cc * G::P * 64);
-    for (int k = k0; k < k1; ++k) {
-      const int ii = k * NW + wave;                      // 1-KiB piece of the chunk
-      if (ii >= T::PPIECES) break;                       // wave-uniform
-      const int off = ii * 1024 + lane * 16;
-      if (off < T::PBYTES)                               // the last piece is partial
-        dma16(src + off, lds_addr(patch0 + buf * T::PB + ii * 1024));
-    }
-  };
-  auto issue_w = [&](int s) {
-    const char* src = reinterpret_cast<const char*>(wsrc + (size_t)s * 3 * 64 * 64);
-    char* slot = wring + (s & 1) * T::WSLOT;
-#pragma unroll
-    for (int k = 0; k < T::WPW; ++k) {
-      const int ii = k * NW + wave;
-      dma16(src + ii * 1024 + lane * 16, lds_addr(slot + ii * 1024));
-    }
-  };
-  const int nsteps = 3 * CC;
-  issue_patch_pieces(0, 0, 0, T::NPW);
-  issue_w(0);
-
-  // per-lane A-fragment pixel bases (cell of GEMM row tile*16 + (lane & 15))
-  int qb[T::MT];
-#pragma unroll
-  for (int i = 0; i < T::MT; ++i) {
-    const int p = tcell<N>((wave * T::MT + i) * 16 + (lane & 15));
-    qb[i] = p >= 0 ? (p / N) * G::W + (p % N) : 0;
-  }
-  // per-lane B-fragment byte offsets (cout row n*16 + (lane & 15), piece lane >> 4)
-  int boff[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int r = n * 16 + (lane & 15);
-    boff[n] = r * 128 + (((lane >> 4) ^ ((r >> 1) & 7)) << 4);
-  }
-  f32x4 acc[T::MT][4];
-#pragma unroll
-  for (int i = 0; i < T::MT; ++i)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the epilogue's residual lines (this chunk's 64 channels of each pixel) are
-  // touched into L2 at the start of the last step, one 4-byte LDS-DMA per
-  // line landing in a dummy LDS area (its latency overlaps the step's MFMAs;
-  // no DMA is issued after it, so no step's vmcnt count changes)
-  auto touch_epilogue = [&]() {
-    if (!a.res) return;
-    const char* r = reinterpret_cast<const char*>(a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride +
-                                                  (size_t)cg * G::P * 64);
-    constexpr int L0 = G::W + 1, NL = (G::N - 1) * G::W + G::N;     // pixel lines of the board's cells
-    if (tid < NL) dma4(r + (size_t)(L0 + tid) * 128, lds_addr(lds) + (uint32_t)(T::LDS - 256));
-  };
-  STAMP_T(tpro);
-
-  // The first A fragments of kernel rows 1 and 2 are read at the end of the
-  // previous step, before its barrier (same patch buffer, no hazard): 26.5 ->
-  // 26.2 us per conv (MZGO_TCONV_NOAPRE=1 to read them after the barrier)
-#ifdef MZGO_TCONV_NOAPRE
-  constexpr bool APRE = false;
-#else
-  constexpr bool APRE = true;
-#endif
-  for (int cc = 0; cc < CC; ++cc) {
-    const bool nextp = cc + 1 < CC;
-    const char* pbuf = patch0 + (cc & 1) * T::PB;
-    bf16x8 afn[T::ADIST > 0 ? T::ADIST : 1][2];
-    // A fragments of group g (tap kx, tile i) of kernel row ky
-    auto frag_a = [&](int kyv, int kx, int i, bf16x8 (&d)[2]) {
-      const int q = qb[i] + kyv * G::W + kx;
-      const int off = q * 128 + (((lane >> 4) ^ tswz(q)) << 4);
-      d[0] = frag_ld(pbuf + off);
-      d[1] = frag_ld(pbuf + (off ^ 64));
-    };
-    auto step = [&](auto kyc) {
-      constexpr int ky = decltype(kyc)::value;
-      const int s = cc * 3 + ky;
-      STAMP_T(ts0);
-      // younger than W(s): the patch pieces of step s-1 (ky-1 of this chunk)
-      int younger = 0;
-      if (ky >= 1 && ky - 1 < 2 && nextp) younger = T::pieces_at(ky - 1, wave);
-      wait_vmcnt_dyn(younger);
-      STAMP_T(ts1);
-      // W(s) (and chunk cc) landed for every wave; this wave's ring reads
-      // done (with APRE the pre-read A fragments, issued last, may stay in flight)
-      if constexpr (APRE && ky > 0) {
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * T::ADIST) : "memory");
-        __builtin_amdgcn_s_barrier();
-      } else {
-        lds_barrier();
-      }
-      STAMP_T(ts2);
-      auto issue_dma = [&]() {
-        if (s + 1 < nsteps) issue_w(s + 1);
-        if (nextp && ky < 2) {
-          constexpr int k0 = ky == 0 ? 0 : (T::NPW + 1) / 2, k1 = ky == 0 ? (T::NPW + 1) / 2 : T::NPW;
-          issue_patch_pieces(cc + 1, (cc + 1) & 1, k0, k1);
-        }
-        if (s == nsteps - 1) touch_epilogue();
-      };
-      // the step's first fragment reads go out before this wave's DMA issue
-      // (26.4 vs 27.0 us per conv; MZGO_TCONV_DMA_FIRST=1 for the old order)
-#ifdef MZGO_TCONV_DMA_FIRST
-      constexpr bool reads_first = false;
-#else
-      constexpr bool reads_first = true;
-#endif
-      if constexpr (!reads_first) issue_dma();
-      // One basic block per step (no per-tile branch: a wave past the last
-      // tile multiplies a clamped tile and drops it in the epilogue), as
-      // groups g = (tap kx, tile i): each group first issues the A fragments
-      // of group g + AD (and at i = 0 the B fragments of tap kx + 1), then
-      // runs its 8 MFMAs on fragments loaded AD groups (B: MT groups) ago.
-      constexpr int NG = 3 * T::MT, AD = T::ADIST;
-      const char* ws = wring + (s & 1) * T::WSLOT;
-      bf16x8 bf[2][4][2], af[AD + 1][2];
-      auto load_b = [&](int kx, bf16x8 (&d)[4][2]) {
-        const char* wt = ws + kx * 64 * 64 * 2;
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          d[n][0] = frag_ld(wt + boff[n]);
-          d[n][1] = frag_ld(wt + (boff[n] ^ 64));
-        }
-      };
-      auto load_a = [&](auto gc) {
-        constexpr int g = decltype(gc)::value, kx = g / T::MT, i = g % T::MT;
-        const int q = qb[i] + ky * G::W + kx;
-        const int off = q * 128 + (((lane >> 4) ^ tswz(q)) << 4);
-        af[g % (AD + 1)][0] = frag_ld(pbuf + off);
-        af[g % (AD + 1)][1] = frag_ld(pbuf + (off ^ 64));
-      };
-      load_b(0, bf[0]);
-      if constexpr (APRE && ky > 0) {
-#pragma unroll
-        for (int g = 0; g < AD; ++g) { af[g][0] = afn[g][0]; af[g][1] = afn[g][1]; }
-      } else {
-        static_for<AD>([&](auto gc) { load_a(gc); });
-      }
-      if constexpr (reads_first) issue_dma();
-      auto group = [&](auto gc) {
-        constexpr int g = decltype(gc)::value, kx = g / T::MT, i = g % T::MT;
-        if constexpr (i == 0 && kx + 1 < 3) load_b(kx + 1, bf[(kx + 1) & 1]);
-        if constexpr (g + AD < NG) load_a(std::integral_constant<int, g + AD>{});
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g % (AD + 1)][0], bf[kx & 1][n][0], acc[i][n], 0, 0, 0);
-          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[g % (AD + 1)][1], bf[kx & 1][n][1], acc[i][n], 0, 0, 0);
-        }
-        // the group's reads first, then its 8 MFMAs, nothing moved across groups
-        constexpr int nrd = (i == 0 && kx + 1 < 3 ? 8 : 0) + (g + AD < NG ? 2 : 0);
-        if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      static_for<NG>([&](auto gc) { group(gc); });
-      if constexpr (APRE && ky < 2) {
-        __builtin_amdgcn_sched_barrier(0);             // the pre-reads are this step's last LDS ops
-#pragma unroll
-        for (int g = 0; g < AD; ++g) frag_a(ky + 1, g / T::MT, g % T::MT, afn[g]);
-      }
-      STAMP_T(ts3);
-#ifdef MZGO_TCONV_STAMPS
-      acc_wait += ts1 - ts0; acc_bar += ts2 - ts1; acc_mfma += ts3 - ts2;
-#endif
-    };
-    step(std::integral_constant<int, 0>{});
-    step(std::integral_constant<int, 1>{});
-    step(std::integral_constant<int, 2>{});
-  }
-  lds_barrier();                                       // every wave's last reads done
-  STAMP_T(tloop);
-
-  // epilogue: the residual pieces and the E[a] rows are fetched first (their
-  // latency overlaps the accumulator staging instead of every item waiting)
-  constexpr int NT = 64 * NW;
-  constexpr int ITEMS = (G::CELLS * 8 + NT - 1) / NT;   // (cell, 8-channel piece) items per thread
-  bf16* out = a.out + (long long)(a.out_idx ? a.out_idx[b] : b) * a.out_stride + (size_t)cg * G::P * 64;
-  const bf16* res = a.res ? a.res + (long long)(a.res_idx ? a.res_idx[b] : b) * a.res_stride + (size_t)cg * G::P * 64
-                          : nullptr;
-  bf16x8 r8[ITEMS];
-  if (res) {
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int idx = tid + k * NT;
-      if (idx < G::CELLS * 8) {
-        const int p = idx >> 3, y = p / N, x = p - y * N;
-        r8[k] = *reinterpret_cast<const bf16x8*>(res + tpix((y + 1) * G::W + (x + 1), idx & 7));
-      }
-    }
-  }
-  // E[a][region][this chunk's 64 couts] -> LDS behind the staging area
-  float* set = reinterpret_cast<float*>(lds) + G::CELLS * 68;
-  constexpr int EK = (9 * 64 + NT - 1) / NT;
-  float ev[EK];
-#pragma unroll
-  for (int k = 0; k < EK; ++k) ev[k] = 0.f;
-  if (a.etab) {
-    const float* eb = a.etab + (size_t)a.act[b] * 9 * CO * 64 + cg * 64;
-#pragma unroll
-    for (int k = 0; k < EK; ++k) {
-      const int i = tid + k * NT;
-      if (i < 9 * 64) ev[k] = eb[(size_t)(i >> 6) * CO * 64 + (i & 63)];
-    }
-  }
-  // accumulators -> fp32 staging [cell][68] (over the patch buffers)
-  float* st = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < T::MT; ++i) {
-    const int ti = wave * T::MT + i;
-    if (ti >= G::TT) break;
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = tcell<N>(ti * 16 + (lane >> 4) * 4 + r);
-        if (p >= 0) st[p * 68 + n * 16 + (lane & 15)] = acc[i][n][r];
-      }
-  }
-  if (a.etab) {
-#pragma unroll
-    for (int k = 0; k < EK; ++k)
-      if (tid + k * NT < 9 * 64) set[tid + k * NT] = ev[k];
-  }
-  __syncthreads();
-  // 8 channels per thread and item: bias, E term, residual, ReLU, bf16 store, head partials
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const int idx = tid + k * NT;
-    if (idx >= G::CELLS * 8) break;
-    const int p = idx >> 3, j = idx & 7;
-    const int y = p / N, x = p - y * N;
-    const int q = (y + 1) * G::W + (x + 1);
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(st + p * 68 + j * 8);
-    const f32x4 s1 = *reinterpret_cast<const f32x4*>(st + p * 68 + j * 8 + 4);
-    float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += sbias[j * 8 + e];
-    if (a.etab) {
-      const int reg = 3 * (y == 0 ? 0 : (y == N - 1 ? 2 : 1)) + (x == 0 ? 0 : (x == N - 1 ? 2 : 1));
-      const f32x4 e0 = *reinterpret_cast<const f32x4*>(set + reg * 64 + j * 8);
-      const f32x4 e1 = *reinterpret_cast<const f32x4*>(set + reg * 64 + j * 8 + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] += e0[e]; v[e + 4] += e1[e]; }
-    }
-    const int off = tpix(q, j);
-    if (res) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += (float)r8[k][e];
-    }
-    bf16x8 o8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o8[e] = (bf16)(v[e] > 0.f ? v[e] : 0.f);
-    *reinterpret_cast<bf16x8*>(out + off) = o8;
-    if (a.headw) {
-      float h[3];
-#pragma unroll
-      for (int hh = 0; hh < 3; ++hh) {
-        float sum = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sum += shw[hh * 64 + j * 8 + e] * (float)o8[e];
-        sum += __shfl_xor(sum, 1);
-        sum += __shfl_xor(sum, 2);
-        sum += __shfl_xor(sum, 4);
-        h[hh] = sum;
-      }
-      if (j == 0) {
-        float* hp = a.hpart + ((size_t)b * CO + cg) * 3 * G::CS + p;
-        hp[0] = h[0];
-        hp[G::CS] = h[1];
-        hp[2 * G::CS] = h[2];
-      }
-    }
-  }
-#ifdef MZGO_TCONV_STAMPS
-  if (lane == 0 && bid < 4096) {
-    const unsigned long long tend = __builtin_amdgcn_s_memtime();
-    const unsigned long long rend = __builtin_amdgcn_s_memrealtime();
-    unsigned long long* g = g_tstamps[bid][wave];
-    g[8] += rend - rstart;
-    g[0] += tend - tstart; g[1] += tpro - tstart; g[2] += acc_wait; g[3] += acc_bar; g[4] += acc_mfma;
-    g[5] += tend - tloop; g[6] += 1;
-  }
-#endif
-}
-
 // ---------------------------------------------------------------------------
 // k_tconv_ks: the same conv with the K dimension split across the two waves
 // of a SIMD.  Wave w = (kh, mg), kh = w >> 2, mg = w & 3: waves kh = 0 take
@@ -519,19 +150,14 @@ __global__ void __launch_bounds__(64 * NW) k_tconv(TConvArgs a) {
 // two halves' partial sums meet once in the epilogue's fp32 staging (kh = 0
 // stores, kh = 1 adds), so a cout's sum is (chain over cin 0-31 of every
 // chunk) + (chain over cin 32-63) -- a different fp32 order, nothing else.
-// Same LDS image, DMA pipeline and barriers as k_tconv.
+// (The M-split k_tconv it replaced -- 3 M tiles x 64 couts per wave, 0.58
+// fragment reads per MFMA -- measured 26.75 vs 26.57 us per conv and was
+// removed in round 5.)
 // ---------------------------------------------------------------------------
-// experiment knobs (A/B builds): MZGO_TCONV_PRIO 1 = s_setprio 1 around every
-// MFMA group, 2 = static priority for waves 4-7.  The timing ablations (wrong
-// results) live in mzgo_diag.hpp, compiled only into diagnostic builds.
-#ifndef MZGO_TCONV_PRIO
-#define MZGO_TCONV_PRIO 0
-#endif
-constexpr int kPrio = MZGO_TCONV_PRIO;
-#ifndef MZGO_TCONV_DMASPREAD
-#define MZGO_TCONV_DMASPREAD 1
-#endif
-constexpr int kDmaSpread = MZGO_TCONV_DMASPREAD;   // > 0: one DMA piece every kDmaSpread MFMA groups
+// (s_setprio around every MFMA group or for waves 4-7 changed nothing, round
+// 3.)  The timing ablations (wrong results) live in mzgo_diag.hpp, compiled
+// only into diagnostic builds.
+constexpr int kDmaSpread = 1;   // one DMA piece every kDmaSpread MFMA groups (2 / 3: 27.05 / 30.9 us, round 3)
 #ifdef MZGO_DIAG_BUILD
 #include "mzgo_diag.hpp"
 #else
@@ -542,14 +168,10 @@ template <int N>
 struct TConvKsGeo {
   typedef TConvGeo<N, 8> T;
   static constexpr int MT = (TGeo<N>::TT + 3) / 4;      // tiles per wave (4 M groups)
-#ifdef MZGO_TCONV_KS_ADIST
-  static constexpr int ADIST = MZGO_TCONV_KS_ADIST;
-#else
   // 1 since round 4: 0 B scratch in k_tconv_ks and k_tconv_chain (2 left the
   // chain kernel 40 B of spills), config 5 1535-1537 -> 1514-1516 ms per move
   // (same call); 3 spills
   static constexpr int ADIST = 1;
-#endif
   static_assert(ADIST >= 1 && ADIST <= 3 * MT, "A prefetch distance");
   static_assert(8 * MT * 2 * 1024 <= 2 * T::PB + 2 * T::WSLOT, "the epilogue's accumulator exchange fits the patch buffers + ring");
 };
@@ -599,14 +221,8 @@ __device__ __forceinline__ void tconv_issue_w0(const TConvArgs& a, int cg) {
 // conv and workgroup, and in k_tconv_chain it was written by other CUs of
 // the XCC since the last read, so no L1 invalidate is needed between layers
 // (MZGO_TCONV_PATCH_L1=1: through L1, with buffer_inv sc0 per layer).
-#ifdef MZGO_TCONV_PATCH_L1
-constexpr bool kPatchL2 = false;
-#else
-constexpr bool kPatchL2 = true;
-#endif
 __device__ __forceinline__ void dma_patch(const void* g, uint32_t lds_dst) {
-  if constexpr (kPatchL2) dma16_l2(g, lds_dst);
-  else dma16(g, lds_dst);
+  dma16_l2(g, lds_dst);
 }
 
 // w0_issued: tconv_issue_w0 ran for this conv already
@@ -629,8 +245,6 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
   const int tid = tid_local(), lane = tid & 63;   // (tid_local: nothing lane-derived is hoisted out of k_tconv_chain's layer loop)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = wave >> 2, mg = wave & 3;
-  if constexpr (kPrio == 2)
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   char* const patch0 = lds;
   char* const wring = lds + 2 * T::PB;
   float* const sbias = reinterpret_cast<float*>(lds + 2 * T::PB + 2 * T::WSLOT);
@@ -782,7 +396,6 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
         if constexpr (g + AD < NG) load_a(std::integral_constant<int, g + AD>{});
         constexpr int nrd = (i == 0 && kx + 1 < 3 ? 4 : 0) + (g + AD < NG ? 1 : 0);
         if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);
-        if constexpr (kPrio == 1) { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_setprio(1); }
           if (!(i == MT - 1 && lastdead)) {
 #pragma unroll
           for (int n = 0; n < 4; ++n)
@@ -790,7 +403,6 @@ __device__ __forceinline__ void tconv_ks_board(const TConvArgs& a, bool w0_issue
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (kPrio == 1) { __builtin_amdgcn_s_setprio(0); __builtin_amdgcn_sched_barrier(0); }
       };
       static_for<NG>([&](auto gc) { group(gc); });
       if constexpr (ky < 2) {
@@ -1059,7 +671,7 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c, const TConvAr
         // local: the data is in the XCC's L2, which the patch reads go to
         // (dma_patch); otherwise this CU's L1 would be invalidated here
         if (local) {
-          if constexpr (!kPatchL2) asm volatile("buffer_inv sc0" ::: "memory");
+          // (the patch reads go past this CU's L1: nothing to invalidate)
         } else {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }

@@ -40,16 +40,7 @@ int tower_stamps_n19(unsigned long long* out);
 template <int N>
 struct TLaunch {
   static hipError_t conv(const TConvArgs& a, hipStream_t s) {
-    // 8 waves (2 per SIMD) unless MZGO_TCONV_WAVES=4 (A/B runs)
-    static const int nw = [] { const char* e = getenv("MZGO_TCONV_WAVES"); return e && atoi(e) == 4 ? 4 : 8; }();
-    // k_tconv_ks unless MZGO_TCONV_KS=0 (the M-split k_tconv, A/B runs)
-    static const bool ks = [] { const char* e = getenv("MZGO_TCONV_KS"); return !(e && atoi(e) == 0); }();
-    if (ks)
-      hipLaunchKernelGGL((k_tconv_ks<N>), dim3(a.nboards * a.co_chunks), dim3(512), 0, s, a);
-    else if (nw == 4)
-      hipLaunchKernelGGL((k_tconv<N, 4>), dim3(a.nboards * a.co_chunks), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_tconv<N, 8>), dim3(a.nboards * a.co_chunks), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_tconv_ks<N>), dim3(a.nboards * a.co_chunks), dim3(512), 0, s, a);
     return hipGetLastError();
   }
   static hipError_t chain(const TConvChain& c, int workgroups, hipStream_t s) {

@@ -238,22 +238,6 @@ def test_tower_config5_shapes_one_move():
         assert gg.invalid_moves(st)[int(r["action"][0])] == 0 or int(r["action"][0]) == N * N
 
 
-@pytest.mark.timeout(300)
-def test_tower_mksplit_kernel_matches_oracle():
-    """The M-split k_tconv (MZGO_TCONV_KS=0: the A/B alternative to the
-    default K-split k_tconv_ks) on the inference parity cases above.  The
-    switch is read once per process, so the cases run in a child process."""
-    import os
-    import subprocess
-    import sys
-    env = dict(os.environ, MZGO_TCONV_KS="0")
-    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__,
-                        "-k", "test_tower_inference_matches_oracle"], env=env, capture_output=True, text=True,
-                       timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert "5 passed" in r.stdout, r.stdout[-1000:]
-
-
 # Config 5's real network (19x19, C=256, 20 blocks) in a search: the engine's
 # tree vs oracle.mcts.MCTS driven by OracleResNet(bf16=True) with the same
 # counter streams and injected noise (SURVEY.md §4, bf16 mode: "root value
