@@ -1779,16 +1779,20 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
     // resumes the walk there (it settles the node's priors and goes on)
     while (sm.t.action == kNeedLogits) {
       const int xn = sm.t.leaf, xd = sm.t.depth;
+      st.lap(0);
       policy_sums_wg<G>(sm.t.logits, pool + (size_t)sm.t.lpar * node_floats,
                         np.etab + (size_t)sm.t.lact * 9 * G::C, np.head_w);
       if (tid_local() == 0) sm.t.lognode = xn;
       ++rows;
       __syncthreads();
+      st.lap(32);
+      if (tid_local() == 0) st.wave_add(34, 1);
       if (wave_id() == 0) {
         const int a = select_leaf<G>(sm.t, T, sp, key, sim, &st, xn, xd);
         if (lane_id_local() == 0) sm.t.action = a;
       }
       __syncthreads();
+      st.lap(33);
     }
     st.lap(0);
     const int a = sm.t.action, leaf = sm.t.leaf, depth = sm.t.depth;

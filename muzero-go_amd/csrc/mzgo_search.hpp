@@ -809,6 +809,14 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
   const int lane = lane_id_local();
   // (node0, depth0): resume a walk that returned kNeedLogits at that node
   int node = node0, depth = depth0, par = -1, pact = -1;
+  if (st) st->lap(35);
+#ifdef MZGO_STAMPS
+  // (stamps builds: the wave's outstanding vector-memory operations -- its
+  // HBM stores -- drained here, so slot 38 is their ack wait and the levels'
+  // slots below hold their loads alone)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (st) st->lap(38);
+#endif
   // a lazily expanded node reached for the first time: its policy sums
   // first (the caller), unless t.logits holds them already
   auto need_logits = [&]() {
@@ -932,7 +940,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     uint64_t any_elig = 0;
 #pragma unroll
     for (int j = 0; j < G::AP; ++j) any_elig |= elig[j];
-    if (st && root) st->lap(24);
+    if (st) st->lap(root ? 24 : 36);
     if (sp.variant == 1) {
       // main.py:318-364 has no terminal test; with no positive-prior child the
       // walk ends without an action and the simulation does nothing (:296)
@@ -961,6 +969,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) t.umask[j] = unexp[j];
       if (root) t.ract = best;
+      if (st) st->lap(37);
       return best;
     }
 
