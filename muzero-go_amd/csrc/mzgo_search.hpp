@@ -829,9 +829,12 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
     const float* pr_row = T.T.prior + (size_t)node * G::A;
     // the newest node's priors may still be in the making (wave 1)
     const bool fresh = !root && node == t.newest;
-    if (fresh)
+    if (fresh) {
+      if (st) st->lap(36);
       while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != node)
         __builtin_amdgcn_s_sleep(1);
+      if (st) st->lap(39);
+    }
     double P[G::AP], rw[G::AP];
     int ch[G::AP], rn[G::AP];
     // all of this node's loads first (one round trip); three sources, chosen
