@@ -433,7 +433,6 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
         __builtin_amdgcn_s_sleep(2);
       unsigned long long t0 = st ? st->now() : 0, t1;
       const int a = __builtin_amdgcn_readfirstlane(L.acts[k]), nid = nid0 + k;
-#ifndef MZGO_EXP_EGLOBAL
       if (a == epre_a) {
 #pragma unroll
         for (int e = 0; e < EP; ++e)
@@ -443,19 +442,13 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
         for (int i = lane; i < E4N; i += 64) ewl[i] = e4[i];
       }
       wave_lds_sync();
-      const float* ewp = W.ew;
-#else
-      const float* ewp = np.etab + (size_t)a * 9 * G::C;
-      (void)ewl; (void)epre_a;
-#endif
       if (st) { t1 = st->now(); st->wave_add(64, t1 - t0); t0 = t1; }
       float rsum, vsum;
-      if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW, !LAZY>(W.xw, yg, ewp, L.hw, plan, rsum, vsum);
-      else expand_wave<G, XL::PROW, !LAZY>(W.xw, L.yc, ewp, L.hw, plan, rsum, vsum);
+      if constexpr (XL::GLOBAL_Y) expand_wave<G, XL::PROW, !LAZY>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+      else expand_wave<G, XL::PROW, !LAZY>(W.xw, L.yc, W.ew, L.hw, plan, rsum, vsum);
       wave_lds_sync();
       epre_a = -1;
       kn = grab();
-#ifndef MZGO_EXP_EGLOBAL
       {
         if (kn < B && __hip_atomic_load(&sm.t.npick, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > kn) {
           epre_a = __builtin_amdgcn_readfirstlane(L.acts[kn]);
@@ -464,7 +457,6 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
           for (int e = 0; e < EP; ++e) epre[e] = e4[lane + 64 * e < E4N ? lane + 64 * e : 0];
         }
       }
-#endif
       if (st) { t1 = st->now(); st->wave_add(65, t1 - t0); t0 = t1; }
       float r, v;
       heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);

@@ -809,7 +809,7 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
   const int lane = lane_id_local();
   // (node0, depth0): resume a walk that returned kNeedLogits at that node
   int node = node0, depth = depth0, par = -1, pact = -1;
-  if (st) st->lap(35);
+  if (st) { st->lap(35); st->wave_add(51, 1); }
 #ifdef MZGO_STAMPS
   // (stamps builds: the wave's outstanding vector-memory operations -- its
   // HBM stores -- drained here, so slot 38 is their ack wait and the levels'
@@ -873,8 +873,10 @@ __device__ __forceinline__ int select_leaf(TreeLds<G>& t, const Acc& T, const Se
         while (__hip_atomic_load(&t.newp_node, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != t.newest)
           __builtin_amdgcn_s_sleep(1);
       float q[G::AP];
+      if (st) st->lap(36);
       settle_lazy<G>(t, const_cast<float*>(pr_row), T.T.child + (size_t)node * G::A, sp.variant, t.fbuf, t.dbuf, q);
       if (lane == 0) atomicAnd(&t.rawp[node >> 5], ~(1u << (node & 31)));
+      if (st) { st->lap(49); st->wave_add(50, 1); }
 #pragma unroll
       for (int j = 0; j < G::AP; ++j) {
         const int a = lane + 64 * j;

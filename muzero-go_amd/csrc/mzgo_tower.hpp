@@ -616,7 +616,9 @@ struct TConvChain {
 };
 
 // bounded wait until (int)(*p - want) >= 0 (thread 0); false on expiry
+// (spin_max < 0, a test hook: every wait expires, ready or not)
 __device__ __forceinline__ bool chain_wait(const unsigned* p, unsigned want, long long spin_max) {
+  if (spin_max < 0) return false;
   for (long long spins = 0; (int)(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0;
        ++spins) {
     if (spins > spin_max) return false;

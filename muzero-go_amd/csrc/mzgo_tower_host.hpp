@@ -141,8 +141,8 @@ struct TowerHost {
       dev = c.dev;
       chains.push_back(std::move(c));
     }
-    // MZGO_TCONV_CHAIN_SPIN: the waits' bound (test hook: a tiny bound makes
-    // them expire, which every API call must then report)
+    // MZGO_TCONV_CHAIN_SPIN: the waits' bound (test hook: a negative bound
+    // makes every wait expire, which every API call must then report)
     long long spin_max = 1ll << 24;
     if (const char* v = getenv("MZGO_TCONV_CHAIN_SPIN")) spin_max = atoll(v);
     const TConvChain ch{dev, (int)L.size(), cflags, cxcc, cseq, cerr, spin_max};

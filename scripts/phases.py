@@ -28,7 +28,7 @@ import torch  # noqa: E402
 PHASES = {
     "representation": [84],                                   # board planes + conv1-3 + heads (per move)
     "root": [85, 4],                                          # root priors + Dirichlet; root batch backups
-    "select": [0, 22, 23, 24, 25, 26, 27, 32, 33, 35, 36, 37, 38, 39],  # select_leaf walks (+ the barrier after
+    "select": [0, 22, 23, 24, 25, 26, 27, 32, 33, 35, 36, 37, 38, 39, 49],  # select_leaf walks (+ the barrier after
                                                               # them; 32/33 a lazy node's policy sums / resumed walk)
     "conv": [1, 6, 7, 20, 21, 29, 30, 52, 53, 54, 60, 81, 82],  # parent / root dynamics convs (Winograd)
     "expand": [2, 3, 5, 40, 41, 42, 43, 61, 62, 69, 70, 71],  # child expansions (heads, priors), picks, backups

@@ -1,0 +1,13 @@
+set -e
+export TMPDIR=/tmp
+for v in stamps; do
+MZGO_LIB=$PWD/muzero-go_amd/mzgo/libmzgo_$v.so timeout -k 10 300 python scripts/phases.py r5q_$v > gpurun_out/r5q_$v.log 2>&1 || { tail -20 gpurun_out/r5q_$v.log; exit 1; }
+done
+python3 - <<'PY'
+import json
+for v in ("stamps",):
+    d = json.load(open(f"gpurun_out/r5q_{v}_phases.json"))
+    s = d["slots_mean_per_game"]
+    print(v, "mean game", round(d["tail"]["mean_game_cycles"]/1e6, 2), "max", round(d["tail"]["max_game_cycles"]/1e6, 2))
+    print({k: s.get(k, 0) for k in ("0", "22", "23", "24", "25", "26", "27", "32", "33", "34", "35", "36", "37", "38", "39", "49", "50", "51", "91")})
+PY

@@ -363,7 +363,8 @@ def test_tower_chain_wait_expiry_is_reported(monkeypatch):
     """An expired k_tconv_chain wait (the launch's results are wrong) is
     reported by the API call that made it -- here a single move() -- as
     MZGO_EHIP, and cleared: the next calls succeed.  The expiry is forced by
-    the test hook MZGO_TCONV_CHAIN_SPIN=-1 (every wait gives up at once)."""
+    the test hook MZGO_TCONV_CHAIN_SPIN=-1 (every wait expires, ready or not:
+    a bound of 0 polls would pass whenever the siblings happened to be done)."""
     import mzgo
     N, C, blocks, G, S = 9, 128, 1, 8, 8
     net = _nets(N, C, blocks, seed=3)[0]
