@@ -309,14 +309,19 @@ def tower_main(args, world, rank, local, cpu_ref):
         from mzgo import distributed as mdist
         mdist.broadcast_weights(net)
     planes = None
+    live = None
     if args.start_move > 0:
         # mid-game (untimed): every game fast-forwarded to move ``start_move`` by
         # self-play at 8 simulations per move on a second engine of the same
-        # network, its boards then loaded into the timed engine's slots
+        # network, its boards then loaded into the timed engine's slots.  A
+        # game that ended during the fast-forward (two passes) is not loaded:
+        # its slot plays from the empty board (games_live_at_start counts the
+        # others) -- the board load carries the position, not a finished game
         ff = mzgo.SelfPlay(net, G, 8, seed=4321, game_base=rank * G)
         ff.reset(epoch=0)
         ff.move(args.start_move)
         planes = ff.engine.board_planes().cpu().numpy()
+        live = [ff.engine.record(g)["status"] == 0 for g in range(G)]
         del ff
         torch.cuda.empty_cache()
     sp = mzgo.SelfPlay(net, G, S, seed=1234, game_base=rank * G)
@@ -324,7 +329,8 @@ def tower_main(args, world, rank, local, cpu_ref):
     sp.reset(epoch=0)
     if planes is not None:
         for g in range(G):
-            eng.board_set(g, planes[g])
+            if live[g]:
+                eng.board_set(g, planes[g])
     for _ in range(args.warmup):
         sp.move()
     torch.cuda.synchronize()
@@ -378,7 +384,9 @@ def tower_main(args, world, rank, local, cpu_ref):
                        "precision": "bf16 MFMA operands, fp32 accumulation, bf16 activations",
                        "start_move": args.start_move,
                        "stones_at_start": None if planes is None else
-                       float((planes[:, 0] + planes[:, 1]).sum() / G)},
+                       float(sum((planes[g, 0] + planes[g, 1]).sum() for g in range(G) if live[g])
+                             / max(sum(live), 1)),
+                       "games_live_at_start": None if live is None else int(sum(live))},
             "roofline": roof,
         }
         if cpu_ref is not None:

@@ -87,8 +87,26 @@ struct TowerHost {
   unsigned long long* cxcc = nullptr;
   int* cerr = nullptr;
   unsigned cseq = 0;
-  struct ChainBuf { std::vector<TConvArgs> host; TConvArgs* dev = nullptr; };
+  // The layer tables: a ring of kChainSlots device slots, each filled from
+  // its own pinned staging copy by an async upload on the launch stream.
+  // Stream order puts an upload after every earlier launch on the stream
+  // (those reading the slot's previous table) and before the launch that
+  // reads it; the event behind the upload guards the staging copy (a host
+  // wait only if a slot comes round again before its last upload ran).  A
+  // call whose table is in a slot already (the dynamics tower's, every
+  // simulation) uploads nothing.  A slot last used on another stream is
+  // reused after that stream drains (calls of one engine on several streams).
+  static constexpr int kChainSlots = 16;
+  struct ChainBuf {
+    std::vector<TConvArgs> host;       // the table in the slot (empty: none)
+    TConvArgs* dev = nullptr;          // device slot, `cap` entries
+    TConvArgs* pin = nullptr;          // pinned staging, `cap` entries
+    int cap = 0;
+    hipEvent_t done = nullptr;         // recorded behind the slot's last upload
+    hipStream_t stream = nullptr;      // of the slot's last launch
+  };
   std::vector<ChainBuf> chains;
+  int chain_next = 0;
   bool chain_ok(int nb) {
     const char* env = getenv("MZGO_TCONV_CHAIN");                // (read per tower: tests switch it)
     if ((env && atoi(env) == 0) || !ts->chain) return false;
@@ -119,28 +137,41 @@ struct TowerHost {
       if ((e = hipMalloc(&cerr, sizeof(int))) != hipSuccess) return e;
       if ((e = hipMemset(cerr, 0, sizeof(int))) != hipSuccess) return e;
     }
-    const TConvArgs* dev = nullptr;
-    for (const ChainBuf& c : chains)
+    if (chains.empty()) chains.resize(kChainSlots);
+    ChainBuf* slot = nullptr;
+    for (ChainBuf& c : chains)
       if (c.host.size() == L.size() && std::memcmp(c.host.data(), L.data(), L.size() * sizeof(TConvArgs)) == 0)
-        dev = c.dev;
-    if (!dev && chains.size() >= 16) {
-      // (inference calls on changing scratch buffers: keep the table cache
-      // bounded; stream-ordered, so wait for launches still reading them)
-      if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-      for (ChainBuf& c : chains) (void)hipFree(c.dev);
-      chains.clear();
-    }
-    if (!dev) {
-      ChainBuf c;
-      c.host = L;
-      if ((e = hipMalloc(&c.dev, L.size() * sizeof(TConvArgs))) != hipSuccess) return e;
-      if ((e = hipMemcpy(c.dev, L.data(), L.size() * sizeof(TConvArgs), hipMemcpyHostToDevice)) != hipSuccess) {
-        (void)hipFree(c.dev);
-        return e;
+        slot = &c;
+    if (!slot) {
+      slot = &chains[chain_next];
+      chain_next = (chain_next + 1) % kChainSlots;
+      ChainBuf& c = *slot;
+      // the staging copy of the slot's last upload: free once that upload ran
+      if (c.done && (e = hipEventSynchronize(c.done)) != hipSuccess) return e;
+      if (c.dev && c.stream != s && (e = hipStreamSynchronize(c.stream)) != hipSuccess) return e;
+      c.host.clear();
+      if (c.cap < (int)L.size()) {
+        // (a larger slot: launches still reading the old one come first)
+        if (c.dev && (e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (c.dev) (void)hipFree(c.dev);
+        if (c.pin) (void)hipHostFree(c.pin);
+        c.dev = nullptr;
+        c.pin = nullptr;
+        c.cap = 0;
+        const int cap = (int)L.size() < 64 ? 64 : (int)L.size();
+        if ((e = hipMalloc(&c.dev, cap * sizeof(TConvArgs))) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&c.pin, cap * sizeof(TConvArgs), hipHostMallocDefault)) != hipSuccess) return e;
+        c.cap = cap;
       }
-      dev = c.dev;
-      chains.push_back(std::move(c));
+      if (!c.done && (e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming)) != hipSuccess) return e;
+      std::memcpy(c.pin, L.data(), L.size() * sizeof(TConvArgs));
+      if ((e = hipMemcpyAsync(c.dev, c.pin, L.size() * sizeof(TConvArgs), hipMemcpyHostToDevice, s)) != hipSuccess)
+        return e;
+      if ((e = hipEventRecord(c.done, s)) != hipSuccess) return e;
+      c.host = L;
     }
+    const TConvArgs* dev = slot->dev;
+    slot->stream = s;
     // MZGO_TCONV_CHAIN_SPIN: the waits' bound (test hook: a negative bound
     // makes every wait expire, which every API call must then report)
     long long spin_max = 1ll << 24;
@@ -164,8 +195,12 @@ struct TowerHost {
     return e;
   }
   void free_chains() {
-    for (ChainBuf& c : chains)
+    for (ChainBuf& c : chains) {
+      if (c.done) (void)hipEventSynchronize(c.done);
       if (c.dev) (void)hipFree(c.dev);
+      if (c.pin) (void)hipHostFree(c.pin);
+      if (c.done) (void)hipEventDestroy(c.done);
+    }
     chains.clear();
     if (cflags) (void)hipFree(cflags);
     if (cxcc) (void)hipFree(cxcc);
