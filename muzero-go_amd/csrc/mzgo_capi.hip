@@ -122,7 +122,12 @@ std::vector<float> pack_conv(const float* W, int COUT, int CIN, bool cog_major, 
 // pos = ((xl/XG)*KP + k)*XG + xl%XG (kWinoXG, KP = CIN/16): one contiguous
 // float4 stream per (cout tile m, xi half h) wave, in the order wino_conv
 // consumes it.
-std::vector<float> pack_wino(const float* W, int COUT, int CIN) {
+// khalf (one-strip boards, wino_conv's KHALF loop): consumption order is
+// K half, xi group, k-position within the half, xi within the group -- the
+// GEMM runs the first half of CIN for every xi before the second, so the
+// rebuilt input's second channel slab is transformed under the first half's
+// MFMAs (wino_conv_rebuilt)
+std::vector<float> pack_wino(const float* W, int COUT, int CIN, bool khalf) {
   static const double G2[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   static const double G3[5][3] = {{0.5, 0, 0},
                                   {1.0 / 6, 1.0 / 6, 1.0 / 6},
@@ -144,7 +149,9 @@ std::vector<float> pack_wino(const float* W, int COUT, int CIN) {
               double u = 0.0;
               for (int a = 0; a < 3; ++a)
                 for (int b = 0; b < 3; ++b) u += G2[i][a] * (double)g[a * 3 + b] * G3[j][b];
-              const int pos = ((xl / kWinoXG) * KP + k) * kWinoXG + xl % kWinoXG;  // consumption order
+              const int KH = KP / 2, kh = k / KH, NG = 10 / kWinoXG;
+              const int pos = khalf ? (((kh * NG + xl / kWinoXG) * KH + k % KH) * kWinoXG + xl % kWinoXG)
+                                    : (((xl / kWinoXG) * KP + k) * kWinoXG + xl % kWinoXG);   // consumption order
               out[((((size_t)m * 2 + h) * L + pos) * 64 + lane) * 4 + e] = (float)u;
             }
   return out;
@@ -250,7 +257,7 @@ struct mzgo_engine {
     const int ksplit = ncg <= 2 ? 2 : 1;
     const bool wino = N == 9 || N == 19;           // Geo::WINO
     auto latent = [&](const char* key, int cout, int cin) {
-      return wino ? pack_wino(sd[key].data(), cout, cin) : pack_conv(sd[key].data(), cout, cin, true, ksplit);
+      return wino ? pack_wino(sd[key].data(), cout, cin, N == 9) : pack_conv(sd[key].data(), cout, cin, true, ksplit);
     };
     parts.push_back(latent("representation.conv2.weight", 64, 64));
     parts.push_back(sd["representation.conv2.bias"]);

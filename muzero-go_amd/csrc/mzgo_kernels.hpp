@@ -257,7 +257,11 @@ template <class G>
 __device__ __forceinline__ void latent_conv_rebuilt(Smem<G>& sm, const NetParams& np, const float* ypar,
                                                     const float* ea, float* dst, Stamp* st = nullptr,
                                                     float* ylds = nullptr, bool par_in_lds = false) {
-  if constexpr (G::WINO) {
+  if constexpr (G::WINO && Wino<G>::NSTRIP == 1) {
+    // (the second channel slab transformed under the GEMM's first K half)
+    wino_conv_rebuilt<G>(sm.u.v, sm.raw, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, ypar, ea, np.w_dyn, np.b_dyn,
+                         dst, st, ylds, par_in_lds ? ylds : nullptr);
+  } else if constexpr (G::WINO) {
     for (int s = 0; s < Wino<G>::NSTRIP; ++s) {
       // par_in_lds: the parent's Y is L.yc (ylds), read from there
       wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s, par_in_lds ? ylds : nullptr);

@@ -301,29 +301,45 @@ __device__ __forceinline__ void wino_input(float* __restrict__ V, float* __restr
 // every slab's Y is read from it into registers first, and the first barrier
 // (before any V store) orders those reads before the transform overwrites it.
 // Typical late in a game: the leaf is a child of the previous batch's leaf.
+// (the steps of wino_input_rebuilt, also run piecewise under the GEMM by
+// wino_conv_rebuilt)
 template <class G, int CIN>
-__device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float* __restrict__ raw,
-                                                   const float* __restrict__ ypar, const float* __restrict__ ea,
-                                                   int strip, const float* ylds = nullptr) {
+struct RebuiltInput {
   typedef Wino<G> W;
   typedef WinoRaw<G> R;
-  constexpr int RS = R::STRIDE, PW = R::PW, PH = R::PH, C4 = CIN / 4;
-  constexpr int F4 = G::WAVES;                          // float4 per cell per slab
+  static constexpr int RS = R::STRIDE, PW = R::PW, PH = R::PH, C4 = CIN / 4;
+  static constexpr int F4 = G::WAVES;                   // float4 per cell per slab
   static_assert(CIN == G::C && G::WAVES % 4 == 0 && CIN % (4 * F4) == 0, "whole slabs, one quad per wave");
-  constexpr int SLABS = CIN / (4 * F4);
-  constexpr int NI = PH * G::N * F4;                    // float4 per slab
-  constexpr int R4 = (NI + G::THREADS - 1) / G::THREADS;
-  const int lane = lane_id_local();
-  const int wave = __builtin_amdgcn_readfirstlane(wave_id());
-  const int t = lane & 15, e = lane >> 4;
-  const int tt = t < W::T ? t : W::T - 1;
-  const int ty = tt / W::TX, tx = tt - ty * W::TX;
-  const int row0 = strip * W::SROWS - 1;
-  if constexpr (SLABS > 2) ylds = nullptr;                // (slabs past the 2nd would read overwritten LDS)
-  const f32x4* Y4 = reinterpret_cast<const f32x4*>(ylds ? ylds : ypar);
-  const f32x4* E4 = reinterpret_cast<const f32x4*>(ea);
+  static constexpr int SLABS = CIN / (4 * F4);
+  static constexpr int NI = PH * G::N * F4;             // float4 per slab
+  static constexpr int R4 = (NI + G::THREADS - 1) / G::THREADS;
+  float* V;
+  float* raw;
+  const f32x4* Y4;
+  const f32x4* E4;
+  bool lds;
+  int row0, wave, t, e, ty, tx;
   f32x4 yv[2][R4], ev[2][R4];                           // slabs k and k + 1
-  auto load = [&](int k, f32x4 (&yd)[R4], f32x4 (&ed)[R4]) {
+  __device__ __forceinline__ RebuiltInput(float* V_, float* raw_, const float* ypar, const float* ea, int strip,
+                                          const float* ylds) {
+    V = V_;
+    raw = raw_;
+    if constexpr (SLABS > 2) ylds = nullptr;            // (slabs past the 2nd would read overwritten LDS)
+    lds = ylds != nullptr;
+    Y4 = reinterpret_cast<const f32x4*>(ylds ? ylds : ypar);
+    E4 = reinterpret_cast<const f32x4*>(ea);
+    const int lane = lane_id_local();
+    wave = __builtin_amdgcn_readfirstlane(wave_id());
+    t = lane & 15;
+    e = lane >> 4;
+    const int tt = t < W::T ? t : W::T - 1;
+    ty = tt / W::TX;
+    tx = tt - ty * W::TX;
+    row0 = strip * W::SROWS - 1;
+  }
+  __device__ __forceinline__ void load(int k) {
+    f32x4 (&yd)[R4] = yv[k & 1];
+    f32x4 (&ed)[R4] = ev[k & 1];
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
       const int i = min(tid_local() + r * G::THREADS, NI - 1);
@@ -333,13 +349,9 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
       yd[r] = Y4[(on ? y * G::N + x : 0) * C4 + F4 * k + q4];
       ed[r] = E4[(ry * 3 + rx) * C4 + F4 * k + q4];
     }
-  };
-  __syncthreads();                                      // the previous conv's epilogue is done with LDS
-  load(0, yv[0], ev[0]);
-  // from LDS: slab 1 too, before the first barrier (V overwrites the copy)
-  if (ylds && SLABS > 1) load(1, yv[1], ev[1]);
-#pragma unroll
-  for (int k = 0; k < SLABS; ++k) {
+  }
+  // slab k's cells, E added and ReLU applied, into the waves' raw planes
+  __device__ __forceinline__ void scatter(int k) {
     f32x4 (&yk)[R4] = yv[k & 1];
     f32x4 (&ek)[R4] = ev[k & 1];
 #pragma unroll
@@ -356,12 +368,69 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
         }
       }
     }
-    // (HBM: the next slab's loads in flight during this slab's transform)
-    if (k + 1 < SLABS && !ylds) load(k + 1, yv[(k + 1) & 1], ev[(k + 1) & 1]);
-    __syncthreads();
+  }
+  // this wave's quad of slab k: raw planes -> V
+  __device__ __forceinline__ void transform(int k) {
     wino_transform_quad<G, CIN>(V, raw + R::base(wave), F4 * k + wave, t, e, ty, tx);
+  }
+  __device__ __forceinline__ void begin() {
+    __syncthreads();                                    // the previous conv's epilogue is done with LDS
+    load(0);
+    // from LDS: slab 1 too, before the first barrier (V overwrites the copy)
+    if (lds && SLABS > 1) load(1);
+  }
+  __device__ __forceinline__ void slab(int k) {
+    scatter(k);
+    // (HBM: the next slab's loads in flight during this slab's transform)
+    if (k + 1 < SLABS && !lds) load(k + 1);
+    __syncthreads();
+    transform(k);
     __syncthreads();                                    // planes read before the next slab / V before the GEMM
   }
+};
+
+template <class G, int CIN>
+__device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float* __restrict__ raw,
+                                                   const float* __restrict__ ypar, const float* __restrict__ ea,
+                                                   int strip, const float* ylds = nullptr) {
+  RebuiltInput<G, CIN> in(V, raw, ypar, ea, strip, ylds);
+  in.begin();
+#pragma unroll
+  for (int k = 0; k < RebuiltInput<G, CIN>::SLABS; ++k) in.slab(k);
+}
+
+// wino_conv of a rebuilt input on one-strip boards (9x9 parent convs), the
+// second channel slab (the GEMM's second K half) scattered and transformed
+// between the first half's MFMA groups instead of before the GEMM: its LDS
+// and VALU work issues under the matrix cores' time.  The same operations as
+// wino_input_rebuilt + wino_conv, so the same bits.
+template <class G>
+struct RebuiltHook {
+  static constexpr bool DEFERS = true;
+  // first-half steps (of KP / 2 * XI / 2 / kWinoXG) after which the scatter,
+  // the barrier before the transform and the transform run
+  static constexpr int kScatter = 1, kBarrier = 5, kTransform = 7;
+  RebuiltInput<G, G::C> in;
+  __device__ __forceinline__ void operator()(int s) {
+    if (s == kScatter) in.scatter(1);
+    else if (s == kBarrier) __syncthreads();
+    else if (s == kTransform) in.transform(1);
+  }
+  __device__ __forceinline__ void finish() { __syncthreads(); }
+};
+template <class G>
+__device__ __forceinline__ void wino_conv_rebuilt(float* V, float* raw, float* red, float* hp, float* outs,
+                                                  float* hfin, const float* __restrict__ ypar,
+                                                  const float* __restrict__ ea, const float* __restrict__ upk,
+                                                  const float* __restrict__ bias, float* __restrict__ out,
+                                                  Stamp* st, float* ylds, const float* ysrc_lds) {
+  static_assert(Wino<G>::NSTRIP == 1 && RebuiltInput<G, G::C>::SLABS == 2, "one strip, two slabs");
+  RebuiltInput<G, G::C> in(V, raw, ypar, ea, 0, ysrc_lds);
+  in.begin();
+  in.slab(0);
+  if (st) st->lap(1);
+  wino_conv<G, G::C, G::C, 0, true, RebuiltHook<G>>(V, red, hp, outs, hfin, upk, bias, out, G::CS, G::CS, nullptr,
+                                                     0, st, ylds, 0, G::C / 16, RebuiltHook<G>{in});
 }
 
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
@@ -388,13 +457,25 @@ __device__ __forceinline__ constexpr float wino_at3(int ox, int j) {
 // cout tiles m0 .. m0 + nm - 1, on waves 0 .. 2 nm - 1; red then needs room
 // for nm tiles only and V is left intact (the next unit reuses it).  Every
 // output is computed by the same operations as in the whole conv.
-template <class G, int CIN, int COUT, int NH, bool YM = false>
+//
+// One-strip boards (KHALF) run the K dimension in two halves, every xi's
+// first half before any second half (pack_wino's khalf order; each xi's
+// chain still adds k = 0 .. KP-1 in order, so the sums are the same bits):
+// hook(s) runs between the MFMA groups of step s of the first half, and a
+// hook that DEFERS the second half's V (wino_conv_rebuilt: that half is
+// transformed during the first) finishes with hook.finish() before it.
+struct WinoNoHook {
+  static constexpr bool DEFERS = false;
+  __device__ void operator()(int) const {}
+  __device__ void finish() const {}
+};
+template <class G, int CIN, int COUT, int NH, bool YM = false, class Hook = WinoNoHook>
 __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp, float* outs, float* hfin,
                                           const float* __restrict__ upk,
                                           const float* __restrict__ bias, float* __restrict__ out,
                                           int out_stride, int out_cells, const float* __restrict__ head_w,
                                           int strip = 0, Stamp* st = nullptr, float* ylds = nullptr, int m0 = 0,
-                                          int nm = COUT / 16) {
+                                          int nm = COUT / 16, Hook hook = Hook{}) {
   typedef Wino<G> W;
   constexpr int CH = CIN / 2, S4 = CH / 16, MT = COUT / 16, XI = W::XI;
   constexpr int OS = W::OUT_STRIDE;
@@ -419,7 +500,83 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   for (int r = 0; r < 4; ++r) bb[r] = active ? bias[m * 16 + kq * 4 + r] : 0.f;
 
   const unsigned long long t_loop = st ? __builtin_amdgcn_s_memtime() : 0ull;
-  if (active) {
+  constexpr bool KHALF = W::NSTRIP == 1;
+  static_assert(!Hook::DEFERS || KHALF, "a deferred second half needs the split K loop");
+  if (KHALF && active) {
+    // (KHALF) all xi's accumulators live across the two K halves
+    constexpr int KH = KP / 2, NG = XH / XG;
+    static_assert(KP % 2 == 0, "two K halves");
+    const f32x4* ap = reinterpret_cast<const f32x4*>(upk) + (size_t)(m * 2 + h) * L * 64 + lane;
+    const f32x4* bp = reinterpret_cast<const f32x4*>(V) + (size_t)h * XH * KP * 64 + lane;
+    auto bidx = [&](int xl, int k) { return (xl * KP + k) * 64; };
+    f32x4 ar[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ar[p] = ap[p * 64];
+    f32x4 bn[XG];
+#pragma unroll
+    for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(q, 0)];
+    f32x4 acc[XH];
+#pragma unroll
+    for (int x = 0; x < XH; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      if (kh == 1 && Hook::DEFERS) {
+        hook.finish();                        // the second half's V is complete
+#pragma unroll
+        for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(q, KH)];
+      }
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        // progress-ordered issue (see below): priority by the group's place in both halves
+        const int pg = kh * NG + g;
+        if (pg < 2) __builtin_amdgcn_s_setprio(3);
+        else if (pg < 4) __builtin_amdgcn_s_setprio(2);
+        else if (pg < 6) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int kk = 0; kk < KH; ++kk) {
+          const int k = kh * KH + kk, s = (kh * NG + g) * KH + kk, pos0 = s * XG;
+          f32x4 a[XG], b[XG];
+#pragma unroll
+          for (int q = 0; q < XG; ++q) { a[q] = ar[(pos0 + q) % PF]; b[q] = bn[q]; }
+          if (kk + 1 < KH) {
+#pragma unroll
+            for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(g * XG + q, k + 1)];
+          } else if (g + 1 < NG) {
+#pragma unroll
+            for (int q = 0; q < XG; ++q) bn[q] = bp[bidx((g + 1) * XG + q, kh * KH)];
+          } else if (kh == 0 && !Hook::DEFERS) {
+#pragma unroll
+            for (int q = 0; q < XG; ++q) bn[q] = bp[bidx(q, KH)];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int q = 0; q < XG; ++q)
+              acc[g * XG + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][e], b[q][e], acc[g * XG + q], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < XG; ++q)
+            if (pos0 + q + PF < L) ar[(pos0 + q) % PF] = ap[(pos0 + q + PF) * 64];
+          __builtin_amdgcn_sched_barrier(0);
+          if (kh == 0) hook(s);
+        }
+      }
+    }
+    // fold along the columns, xi ascending as below
+#pragma unroll
+    for (int xl = 0; xl < XH; ++xl) {
+      const int il = xl / 5, j = xl % 5;
+      const f32x4 mv = acc[xl];
+#pragma unroll
+      for (int ox = 0; ox < 3; ++ox) {
+        const float cf = wino_at3(ox, j);
+        if (cf == 1.f) yp[il * 3 + ox] += mv;
+        else if (cf == -1.f) yp[il * 3 + ox] -= mv;
+        else if (cf != 0.f) yp[il * 3 + ox] += cf * mv;
+      }
+    }
+  } else if (!KHALF && active) {
     // this wave: xi in [h*XH, h*XH + XH), all CIN (KP float4 k-positions per xi).
     // A stream: positions pos = ((g*KP + k)*XG + q) for local xi g*XG + q, in
     // consumption order (pack_wino), PF float4 registers ahead
