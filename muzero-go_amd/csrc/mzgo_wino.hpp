@@ -407,9 +407,11 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
 template <class G>
 struct RebuiltHook {
   static constexpr bool DEFERS = true;
-  // first-half steps (of KP / 2 * XI / 2 / kWinoXG) after which the scatter,
-  // the barrier before the transform and the transform run
-  static constexpr int kScatter = 1, kBarrier = 5, kTransform = 7;
+  // first-half steps (of KP / 2 * XI / 2 / kWinoXG = 15 at 9x9) after which
+  // the scatter, the barrier before the transform and the transform run
+  // (measured, same call: (2, 7, 10) 81.4-81.6 M sims/s, (2, 6, 9) 81.3,
+  // (4, 10, 12) 81.3-81.4, (1, 5, 7) 81.0, (0, 3, 4) 80.4-80.7)
+  static constexpr int kScatter = 2, kBarrier = 7, kTransform = 10;
   RebuiltInput<G, G::C> in;
   __device__ __forceinline__ void operator()(int s) {
     if (s == kScatter) in.scatter(1);
