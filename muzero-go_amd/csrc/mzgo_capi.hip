@@ -257,7 +257,7 @@ struct mzgo_engine {
     const int ksplit = ncg <= 2 ? 2 : 1;
     const bool wino = N == 9 || N == 19;           // Geo::WINO
     auto latent = [&](const char* key, int cout, int cin) {
-      return wino ? pack_wino(sd[key].data(), cout, cin, N == 9) : pack_conv(sd[key].data(), cout, cin, true, ksplit);
+      return wino ? pack_wino(sd[key].data(), cout, cin, true) : pack_conv(sd[key].data(), cout, cin, true, ksplit);
     };
     parts.push_back(latent("representation.conv2.weight", 64, 64));
     parts.push_back(sd["representation.conv2.bias"]);

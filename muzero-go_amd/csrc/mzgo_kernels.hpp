@@ -262,13 +262,9 @@ __device__ __forceinline__ void latent_conv_rebuilt(Smem<G>& sm, const NetParams
     wino_conv_rebuilt<G>(sm.u.v, sm.raw, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, ypar, ea, np.w_dyn, np.b_dyn,
                          dst, st, ylds, par_in_lds ? ylds : nullptr);
   } else if constexpr (G::WINO) {
-    for (int s = 0; s < Wino<G>::NSTRIP; ++s) {
-      // par_in_lds: the parent's Y is L.yc (ylds), read from there
-      wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s, par_in_lds ? ylds : nullptr);
-      if (st) st->lap(1);
-      wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
-                                        dst, G::CS, G::CS, nullptr, s, st, ylds);
-    }
+    for (int s = 0; s < Wino<G>::NSTRIP; ++s)
+      wino_conv_rebuilt<G>(sm.u.v, sm.raw, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, ypar, ea, np.w_dyn,
+                           np.b_dyn, dst, st, ylds, par_in_lds ? ylds : nullptr, s);
     if constexpr (Wino<G>::NSTRIP > 1) __syncthreads();
   }
 }
@@ -645,10 +641,15 @@ __device__ __forceinline__ int conv_strips(Smem<G>& sm, const NetParams& np, con
   int mine = 0;
   if constexpr (G::WINO) {
     for (int s; (s = job_claim(sm, J, bseq, Wino<G>::NSTRIP, 1)) >= 0; ++mine) {
-      if (ypar) wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, s);
-      else wino_input<G, G::C>(sm.u.v, sm.raw, src, G::CS, nullptr, s);
-      wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
-                                         dst, G::CS, G::CS, nullptr, s);
+      if (ypar) {
+        // (the second channel slab transformed under the GEMM's first K half)
+        wino_conv_rebuilt<G>(sm.u.v, sm.raw, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, ypar, ea, np.w_dyn,
+                             np.b_dyn, dst, nullptr, nullptr, nullptr, s);
+      } else {
+        wino_input<G, G::C>(sm.u.v, sm.raw, src, G::CS, nullptr, s);
+        wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.u.x.red, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn,
+                                           dst, G::CS, G::CS, nullptr, s);
+      }
     }
   }
   __syncthreads();

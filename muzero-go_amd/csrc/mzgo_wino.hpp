@@ -425,14 +425,14 @@ __device__ __forceinline__ void wino_conv_rebuilt(float* V, float* raw, float* r
                                                   float* hfin, const float* __restrict__ ypar,
                                                   const float* __restrict__ ea, const float* __restrict__ upk,
                                                   const float* __restrict__ bias, float* __restrict__ out,
-                                                  Stamp* st, float* ylds, const float* ysrc_lds) {
-  static_assert(Wino<G>::NSTRIP == 1 && RebuiltInput<G, G::C>::SLABS == 2, "one strip, two slabs");
-  RebuiltInput<G, G::C> in(V, raw, ypar, ea, 0, ysrc_lds);
+                                                  Stamp* st, float* ylds, const float* ysrc_lds, int strip = 0) {
+  static_assert(RebuiltInput<G, G::C>::SLABS == 2, "two slabs");
+  RebuiltInput<G, G::C> in(V, raw, ypar, ea, strip, ysrc_lds);
   in.begin();
   in.slab(0);
   if (st) st->lap(1);
   wino_conv<G, G::C, G::C, 0, true, RebuiltHook<G>>(V, red, hp, outs, hfin, upk, bias, out, G::CS, G::CS, nullptr,
-                                                     0, st, ylds, 0, G::C / 16, RebuiltHook<G>{in});
+                                                     strip, st, ylds, 0, G::C / 16, RebuiltHook<G>{in});
 }
 
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
@@ -502,7 +502,7 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
   for (int r = 0; r < 4; ++r) bb[r] = active ? bias[m * 16 + kq * 4 + r] : 0.f;
 
   const unsigned long long t_loop = st ? __builtin_amdgcn_s_memtime() : 0ull;
-  constexpr bool KHALF = W::NSTRIP == 1;
+  constexpr bool KHALF = true;                // (every Winograd board: pack_wino's khalf order)
   static_assert(!Hook::DEFERS || KHALF, "a deferred second half needs the split K loop");
   if (KHALF && active) {
     // (KHALF) all xi's accumulators live across the two K halves
