@@ -696,9 +696,10 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
 // that sees a helper registered publishes its next parent conv as a job of
 // kTailUnits units -- unit u = cout tiles 2u, 2u + 1 (wino_conv's m0 / nm) --
 // claims units itself too (it never waits for a helper to start), waits for
-// all, and loads the whole Y from L2 into its LDS copy.  Every unit computes
-// the full Winograd input (wino_input_rebuilt from the parent's Y in the pool)
-// once per job and its tiles' GEMM + epilogue exactly as the whole conv does,
+// all, and loads the whole Y from L2 into its LDS copy.  Every workgroup
+// computes the full Winograd input (from the parent's Y in the pool; the
+// second slab under its first unit's GEMM, wino_conv_rebuilt) once per job and
+// each unit's tiles' GEMM + epilogue exactly as the whole conv does,
 // so the records do not depend on who computed what (MZGO_TAIL_HELPERS=0 A/B).
 // Hand-offs: the job machinery above (release / relaxed flag / acquire).
 // ---------------------------------------------------------------------------
@@ -724,9 +725,12 @@ __device__ __forceinline__ int tail_conv_units(Smem<G>& sm, const NetParams& np,
   int mine = 0;
   if constexpr (TailConvs<G>::value) {
     for (int u; (u = job_claim(sm, J, bseq, kTailUnits, 1)) >= 0; ++mine) {
-      if (mine == 0) wino_input_rebuilt<G, G::C>(sm.u.v, sm.raw, ypar, ea, 0, ylds_par);
-      wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.raw, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn, dst,
-                                        G::CS, G::CS, nullptr, 0, nullptr, nullptr, 2 * u, 2);
+      if (mine == 0)   // (the second slab transformed under the first unit's GEMM, by every wave)
+        wino_conv_rebuilt<G>(sm.u.v, sm.raw, sm.raw, sm.u.x.hp, sm.u.x.outs, sm.hfin, ypar, ea, np.w_dyn, np.b_dyn,
+                             dst, nullptr, nullptr, ylds_par, 0, 2 * u, 2);
+      else
+        wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.raw, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn, dst,
+                                          G::CS, G::CS, nullptr, 0, nullptr, nullptr, 2 * u, 2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's Y stores done
     __syncthreads();

@@ -425,14 +425,15 @@ __device__ __forceinline__ void wino_conv_rebuilt(float* V, float* raw, float* r
                                                   float* hfin, const float* __restrict__ ypar,
                                                   const float* __restrict__ ea, const float* __restrict__ upk,
                                                   const float* __restrict__ bias, float* __restrict__ out,
-                                                  Stamp* st, float* ylds, const float* ysrc_lds, int strip = 0) {
+                                                  Stamp* st, float* ylds, const float* ysrc_lds, int strip = 0,
+                                                  int m0 = 0, int nm = G::C / 16) {
   static_assert(RebuiltInput<G, G::C>::SLABS == 2, "two slabs");
   RebuiltInput<G, G::C> in(V, raw, ypar, ea, strip, ysrc_lds);
   in.begin();
   in.slab(0);
   if (st) st->lap(1);
   wino_conv<G, G::C, G::C, 0, true, RebuiltHook<G>>(V, red, hp, outs, hfin, upk, bias, out, G::CS, G::CS, nullptr,
-                                                     strip, st, ylds, 0, G::C / 16, RebuiltHook<G>{in});
+                                                     strip, st, ylds, m0, nm, RebuiltHook<G>{in});
 }
 
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
@@ -578,6 +579,13 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
         else if (cf != 0.f) yp[il * 3 + ox] += cf * mv;
       }
     }
+  } else if (KHALF && Hook::DEFERS) {
+    // waves without a cout tile (m0 / nm): their share of the hook's work,
+    // at the same barriers as the active waves
+    constexpr int KH = KP / 2, NG = XH / XG;
+#pragma unroll
+    for (int s = 0; s < NG * KH; ++s) hook(s);
+    hook.finish();
   } else if (!KHALF && active) {
     // this wave: xi in [h*XH, h*XH + XH), all CIN (KP float4 k-positions per xi).
     // A stream: positions pos = ((g*KP + k)*XG + q) for local xi g*XG + q, in
