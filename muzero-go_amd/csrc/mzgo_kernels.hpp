@@ -703,8 +703,15 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
 // so the records do not depend on who computed what (MZGO_TAIL_HELPERS=0 A/B).
 // Hand-offs: the job machinery above (release / relaxed flag / acquire).
 // ---------------------------------------------------------------------------
-constexpr int kTailUnits = 3;
-constexpr unsigned kTailHelpers = 2;
+#ifndef MZGO_TAIL_UNITS
+#define MZGO_TAIL_UNITS 3
+#endif
+#ifndef MZGO_TAIL_HELPERS_MAX
+#define MZGO_TAIL_HELPERS_MAX 2
+#endif
+constexpr int kTailUnits = MZGO_TAIL_UNITS;
+constexpr unsigned kTailHelpers = MZGO_TAIL_HELPERS_MAX;
+constexpr int kTailTiles = 6 / kTailUnits;     // cout tiles per unit
 constexpr int kJobTailConv = 6;        // JobView info[4] of a tail conv job
 
 template <class G>
@@ -727,10 +734,10 @@ __device__ __forceinline__ int tail_conv_units(Smem<G>& sm, const NetParams& np,
     for (int u; (u = job_claim(sm, J, bseq, kTailUnits, 1)) >= 0; ++mine) {
       if (mine == 0)   // (the second slab transformed under the first unit's GEMM, by every wave)
         wino_conv_rebuilt<G>(sm.u.v, sm.raw, sm.raw, sm.u.x.hp, sm.u.x.outs, sm.hfin, ypar, ea, np.w_dyn, np.b_dyn,
-                             dst, nullptr, nullptr, ylds_par, 0, 2 * u, 2);
+                             dst, nullptr, nullptr, ylds_par, 0, kTailTiles * u, kTailTiles);
       else
         wino_conv<G, G::C, G::C, 0, true>(sm.u.v, sm.raw, sm.u.x.hp, sm.u.x.outs, sm.hfin, np.w_dyn, np.b_dyn, dst,
-                                          G::CS, G::CS, nullptr, 0, nullptr, nullptr, 2 * u, 2);
+                                          G::CS, G::CS, nullptr, 0, nullptr, nullptr, kTailTiles * u, kTailTiles);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's Y stores done
     __syncthreads();

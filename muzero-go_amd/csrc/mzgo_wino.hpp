@@ -399,43 +399,6 @@ __device__ __forceinline__ void wino_input_rebuilt(float* __restrict__ V, float*
   for (int k = 0; k < RebuiltInput<G, CIN>::SLABS; ++k) in.slab(k);
 }
 
-// wino_conv of a rebuilt input on one-strip boards (9x9 parent convs), the
-// second channel slab (the GEMM's second K half) scattered and transformed
-// between the first half's MFMA groups instead of before the GEMM: its LDS
-// and VALU work issues under the matrix cores' time.  The same operations as
-// wino_input_rebuilt + wino_conv, so the same bits.
-template <class G>
-struct RebuiltHook {
-  static constexpr bool DEFERS = true;
-  // first-half steps (of KP / 2 * XI / 2 / kWinoXG = 15 at 9x9) after which
-  // the scatter, the barrier before the transform and the transform run
-  // (measured, same call: (2, 7, 10) 81.4-81.6 M sims/s, (2, 6, 9) 81.3,
-  // (4, 10, 12) 81.3-81.4, (1, 5, 7) 81.0, (0, 3, 4) 80.4-80.7)
-  static constexpr int kScatter = 2, kBarrier = 7, kTransform = 10;
-  RebuiltInput<G, G::C> in;
-  __device__ __forceinline__ void operator()(int s) {
-    if (s == kScatter) in.scatter(1);
-    else if (s == kBarrier) __syncthreads();
-    else if (s == kTransform) in.transform(1);
-  }
-  __device__ __forceinline__ void finish() { __syncthreads(); }
-};
-template <class G>
-__device__ __forceinline__ void wino_conv_rebuilt(float* V, float* raw, float* red, float* hp, float* outs,
-                                                  float* hfin, const float* __restrict__ ypar,
-                                                  const float* __restrict__ ea, const float* __restrict__ upk,
-                                                  const float* __restrict__ bias, float* __restrict__ out,
-                                                  Stamp* st, float* ylds, const float* ysrc_lds, int strip = 0,
-                                                  int m0 = 0, int nm = G::C / 16) {
-  static_assert(RebuiltInput<G, G::C>::SLABS == 2, "two slabs");
-  RebuiltInput<G, G::C> in(V, raw, ypar, ea, strip, ysrc_lds);
-  in.begin();
-  in.slab(0);
-  if (st) st->lap(1);
-  wino_conv<G, G::C, G::C, 0, true, RebuiltHook<G>>(V, red, hp, outs, hfin, upk, bias, out, G::CS, G::CS, nullptr,
-                                                     strip, st, ylds, m0, nm, RebuiltHook<G>{in});
-}
-
 // AT2 (2 x 4) and AT3 (3 x 5) of the output transform
 __device__ __forceinline__ constexpr float wino_at2(int oy, int i) {
   return oy == 0 ? (i < 3 ? 1.f : 0.f) : (i == 0 ? 0.f : (i == 2 ? -1.f : 1.f));
@@ -825,6 +788,43 @@ __device__ __forceinline__ void wino_conv(const float* V, float* red, float* hp,
     }
   }
   // no barrier: a caller that reads ``out`` (or hfin) back synchronises first
+}
+
+// wino_conv of a rebuilt input on one-strip boards (9x9 parent convs), the
+// second channel slab (the GEMM's second K half) scattered and transformed
+// between the first half's MFMA groups instead of before the GEMM: its LDS
+// and VALU work issues under the matrix cores' time.  The same operations as
+// wino_input_rebuilt + wino_conv, so the same bits.
+template <class G>
+struct RebuiltHook {
+  static constexpr bool DEFERS = true;
+  // first-half steps (of KP / 2 * XI / 2 / kWinoXG = 15 at 9x9) after which
+  // the scatter, the barrier before the transform and the transform run
+  // (measured, same call: (2, 7, 10) 81.4-81.6 M sims/s, (2, 6, 9) 81.3,
+  // (4, 10, 12) 81.3-81.4, (1, 5, 7) 81.0, (0, 3, 4) 80.4-80.7)
+  static constexpr int kScatter = 2, kBarrier = 7, kTransform = 10;
+  RebuiltInput<G, G::C> in;
+  __device__ __forceinline__ void operator()(int s) {
+    if (s == kScatter) in.scatter(1);
+    else if (s == kBarrier) __syncthreads();
+    else if (s == kTransform) in.transform(1);
+  }
+  __device__ __forceinline__ void finish() { __syncthreads(); }
+};
+template <class G>
+__device__ __forceinline__ void wino_conv_rebuilt(float* V, float* raw, float* red, float* hp, float* outs,
+                                                  float* hfin, const float* __restrict__ ypar,
+                                                  const float* __restrict__ ea, const float* __restrict__ upk,
+                                                  const float* __restrict__ bias, float* __restrict__ out,
+                                                  Stamp* st, float* ylds, const float* ysrc_lds, int strip = 0,
+                                                  int m0 = 0, int nm = G::C / 16) {
+  static_assert(RebuiltInput<G, G::C>::SLABS == 2, "two slabs");
+  RebuiltInput<G, G::C> in(V, raw, ypar, ea, strip, ysrc_lds);
+  in.begin();
+  in.slab(0);
+  if (st) st->lap(1);
+  wino_conv<G, G::C, G::C, 0, true, RebuiltHook<G>>(V, red, hp, outs, hfin, upk, bias, out, G::CS, G::CS, nullptr,
+                                                     strip, st, ylds, m0, nm, RebuiltHook<G>{in});
 }
 
 }  // namespace mzgo
