@@ -703,14 +703,14 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
 // so the records do not depend on who computed what (MZGO_TAIL_HELPERS=0 A/B).
 // Hand-offs: the job machinery above (release / relaxed flag / acquire).
 // ---------------------------------------------------------------------------
-#ifndef MZGO_TAIL_UNITS
-#define MZGO_TAIL_UNITS 3
+#ifdef MZGO_DIAG_BUILD
+#include "mzgo_diag.hpp"                    // (the granularity A/B)
+constexpr int kTailUnits = kDiagTailUnits;
+constexpr unsigned kTailHelpers = kDiagTailHelpers;
+#else
+constexpr int kTailUnits = 3;
+constexpr unsigned kTailHelpers = 2;
 #endif
-#ifndef MZGO_TAIL_HELPERS_MAX
-#define MZGO_TAIL_HELPERS_MAX 2
-#endif
-constexpr int kTailUnits = MZGO_TAIL_UNITS;
-constexpr unsigned kTailHelpers = MZGO_TAIL_HELPERS_MAX;
 constexpr int kTailTiles = 6 / kTailUnits;     // cout tiles per unit
 constexpr int kJobTailConv = 6;        // JobView info[4] of a tail conv job
 
