@@ -8,12 +8,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Diagnostic switches (stage knock-outs and timing ablations, which change
-// results; tuning A/Bs) exist only in diagnostic builds (mzgo_diag.hpp): the
-// product library refuses to compile with any of them.
-#if !defined(MZGO_DIAG_BUILD) && (defined(MZGO_TCONV_ABL_NODMA) || defined(MZGO_TCONV_ABL_NOBAR) || \
-                                 defined(MZGO_TAIL_UNITS) || defined(MZGO_TAIL_HELPERS_MAX))
-#error "diagnostic switch without -DMZGO_DIAG_BUILD (diagnostic builds: scripts/build_variant.sh)"
+// Diagnostic switches that change results (stage knock-outs, timing
+// ablations) exist only in diagnostic builds (mzgo_diag.hpp): the product
+// library refuses to compile with any of them.
+#if !defined(MZGO_DIAG_BUILD) && (defined(MZGO_TCONV_ABL_NODMA) || defined(MZGO_TCONV_ABL_NOBAR))
+#error "wrong-result diagnostic switch without -DMZGO_DIAG_BUILD (diagnostic builds: scripts/build_variant.sh)"
 #endif
 
 namespace mzgo {

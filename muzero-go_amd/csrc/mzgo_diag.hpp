@@ -20,15 +20,3 @@ constexpr bool kAblNoBar = true;
 constexpr bool kAblNoBar = false;
 #endif
 
-// 9x9 tail conv jobs: units per job (6 / units cout tiles each) and helpers
-// per game (same results; the granularity A/B of DESIGN §7 (i))
-#ifdef MZGO_TAIL_UNITS
-constexpr int kDiagTailUnits = MZGO_TAIL_UNITS;
-#else
-constexpr int kDiagTailUnits = 3;
-#endif
-#ifdef MZGO_TAIL_HELPERS_MAX
-constexpr unsigned kDiagTailHelpers = MZGO_TAIL_HELPERS_MAX;
-#else
-constexpr unsigned kDiagTailHelpers = 2;
-#endif

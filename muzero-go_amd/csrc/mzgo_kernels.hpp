@@ -518,6 +518,9 @@ __host__ __device__ constexpr int job_bytes(int A) {
   return 512 + 2 * ((A * 8 + 255) / 256 * 256) + (A + 255) / 256 * 256 + ((A - 1 + 15) / 16 * 16 * 12 + 255) / 256 * 256;
 }
 constexpr unsigned kJobExit = 0xFFFFFFFFu;
+// s_sleep units (64 clocks) between polls: a game waiting for its job's units,
+// a helper waiting for the next job ((1, 2) measured the same)
+constexpr int kJobWaitSleep = 4, kJobPollSleep = 8;
 struct JobView {
   unsigned char* base;
   __device__ unsigned long long* claim() const { return reinterpret_cast<unsigned long long*>(base); }
@@ -597,7 +600,7 @@ __device__ __forceinline__ void job_wait(const JobView& J, int mine, int total) 
   if (tid_local() == 0) {
     unsigned d = __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
     while (d < (unsigned)total) {
-      __builtin_amdgcn_s_sleep(4);
+      __builtin_amdgcn_s_sleep(kJobWaitSleep);
       d = __hip_atomic_load(J.done(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -703,14 +706,8 @@ __device__ __forceinline__ void conv_shared(Smem<G>& sm, const NetParams& np, co
 // so the records do not depend on who computed what (MZGO_TAIL_HELPERS=0 A/B).
 // Hand-offs: the job machinery above (release / relaxed flag / acquire).
 // ---------------------------------------------------------------------------
-#ifdef MZGO_DIAG_BUILD
-#include "mzgo_diag.hpp"                    // (the granularity A/B)
-constexpr int kTailUnits = kDiagTailUnits;
-constexpr unsigned kTailHelpers = kDiagTailHelpers;
-#else
-constexpr int kTailUnits = 3;
+constexpr int kTailUnits = 3;           // (granularity measured)
 constexpr unsigned kTailHelpers = 2;
-#endif
 constexpr int kTailTiles = 6 / kTailUnits;     // cout tiles per unit
 constexpr int kJobTailConv = 6;        // JobView info[4] of a tail conv job
 
@@ -816,7 +813,7 @@ __device__ __forceinline__ void tail_help(Smem<G>& sm, const NetParams& np_a, co
         if (tid_local() == 0) {
           unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 24); ++spins) {
-            __builtin_amdgcn_s_sleep(8);
+            __builtin_amdgcn_s_sleep(kJobPollSleep);
             s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           int expired = 0;
@@ -1606,7 +1603,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     if (tid_local() == 0) {
       unsigned s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (long long spins = 0; (s == last || s == 0) && spins < (1ll << 26); ++spins) {
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(kJobPollSleep);
         s = __hip_atomic_load(J.seq(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (s == last || s == 0) s = kJobExit;           // (bounded wait: give up)
