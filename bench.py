@@ -545,7 +545,7 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="oracle processes for cpu_baseline (the GPU box's CPU share is 16)")
     args = ap.parse_args()
-    defaults = {2: dict(board_size=9, games=256, sims=200, latent_dim=96, steps=10, warmup=1),
+    defaults = {2: dict(board_size=9, games=256, sims=200, latent_dim=96, steps=20, warmup=3),
                 5: dict(board_size=19, games=64, sims=1600, latent_dim=256, steps=2, warmup=1)}[args.config]
     for k, v in defaults.items():
         if getattr(args, k) is None:
