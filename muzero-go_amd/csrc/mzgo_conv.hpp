@@ -287,23 +287,29 @@ __device__ __forceinline__ void dma16(const void* g, uint32_t lds_dst) {
       : "memory");
 }
 
-// 4 bytes per lane (LDS destination base + lane*4): an L2 prefetch whose data
-// lands in a dummy LDS area
-// dma16 with sc0: the read is served from L2, never from this CU's L1 (data
-// that other CUs of the XCC wrote since: k_tconv_chain's layer hand-offs)
+// dma16 with sc1 (agent scope): the read misses this CU's L1 and is served by
+// the XCC's L2, so it sees what other CUs of the XCC stored there since
+// (k_tconv_chain's same-XCC layer hand-offs).  Until round 6 this was `sc0`,
+// which is WORKGROUP scope: an sc0 load hits L1 like a plain one and could
+// return a line cached before a sibling CU rewrote it (tools/l1_visibility_probe,
+// DESIGN.md §7).  Same speed: config 5 1526.7-1528.1 ms per move with sc1,
+// 1528.0-1528.2 with sc0, 1527.5-1528.6 with "sc0 sc1", 1533-1534 with nt
+// (profiles/r6b_patch_policy_ab.txt, one call).
 __device__ __forceinline__ void dma16_l2(const void* g, uint32_t lds_dst) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off sc0\n\t"
+      "global_load_lds_dwordx4 %1, off sc1\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(g), "s"(lds_dst)
       : "memory");
 }
 
+// 4 bytes per lane (LDS destination base + lane*4): an L2 prefetch whose data
+// lands in a dummy LDS area
 __device__ __forceinline__ void dma4(const void* g, uint32_t lds_dst) {
   uint32_t keep;
   asm volatile(

@@ -591,6 +591,7 @@ __device__ __forceinline__ void job_publish(const JobView& J, unsigned bseq) {
   __syncthreads();
   if (tid_local() == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
     __hip_atomic_store(J.seq(), bseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -854,6 +855,7 @@ __device__ __forceinline__ void tail_help(Smem<G>& sm, const NetParams& np_a, co
 #endif
         if (tid_local() == 0 && mine > 0) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
           __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -1640,6 +1642,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       __syncthreads();
       if (tid_local() == 0 && mine > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
         __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       continue;
@@ -1654,6 +1657,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       __syncthreads();
       if (tid_local() == 0 && mine > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
         __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       continue;
@@ -1668,6 +1672,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
       __syncthreads();
       if (tid_local() == 0 && mine > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
         __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       continue;
@@ -1683,6 +1688,7 @@ __device__ __forceinline__ void helper_loop(Smem<G>& sm, const NetParams& np_a, 
     __syncthreads();
     if (tid_local() == 0 && mine > 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
       __hip_atomic_fetch_add(J.done(), (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

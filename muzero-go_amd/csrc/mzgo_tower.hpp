@@ -217,10 +217,12 @@ __device__ __forceinline__ void tconv_issue_w0(const TConvArgs& a, int cg) {
   }
 }
 
-// The patch pieces bypass L1 (dma16_l2): an input chunk is read once per
-// conv and workgroup, and in k_tconv_chain it was written by other CUs of
-// the XCC since the last read, so no L1 invalidate is needed between layers
-// (MZGO_TCONV_PATCH_L1=1: through L1, with buffer_inv sc0 per layer).
+// The patch pieces bypass L1 (dma16_l2, agent-scope `sc1` loads): an input
+// chunk is read once per conv and workgroup, and in k_tconv_chain it was
+// written by other CUs of the XCC since the last read, so no L1 invalidate is
+// needed between layers.  (Round 5 issued them `sc0`, workgroup scope, which
+// hits L1 like a plain load: correct only because each conv streams far more
+// than the 32 KiB L1 between two reads of a buffer)
 __device__ __forceinline__ void dma_patch(const void* g, uint32_t lds_dst) {
   dma16_l2(g, lds_dst);
 }
@@ -600,8 +602,11 @@ __global__ void __launch_bounds__(512) k_tconv_ks(TConvArgs a) {
 // tconv_slot) the board's hand-offs stay inside that XCC's L2, the
 // coherence point of its CUs: the producer drains its stores to L2 and
 // stores the flag, the consumer sees the flag and reads the patch from L2
-// past its CU's L1 (dma_patch).  A board split over XCCs keeps the agent-scope
-// protocol.  Replaces 2 blocks + 1 launches per tower: no per-launch
+// past its CU's L1 (dma_patch: `sc1` loads).  Every other load of the chain
+// reads bytes no other workgroup writes in the launch (weights, bias, E
+// table, and the residual: chunk cg of a board is only ever written by
+// workgroup (b, cg), whose own earlier stores its L1 reflects).  A board split
+// over XCCs keeps the agent-scope protocol.  Replaces 2 blocks + 1 launches per tower: no per-launch
 // dispatch ramp and drain, and a board starts its next conv as soon as its
 // own chunks are done.
 // ---------------------------------------------------------------------------
@@ -671,11 +676,11 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c, const TConvAr
           bad = true;
         }
         // local: the data is in the XCC's L2, which the patch reads go to
-        // (dma_patch); otherwise this CU's L1 would be invalidated here
-        if (local) {
-          // (the patch reads go past this CU's L1: nothing to invalidate)
-        } else {
+        // (dma_patch, sc1 loads past this CU's L1); otherwise the agent-scope
+        // acquire (buffer_inv sc1) drops this CU's stale lines
+        if (!local) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate done before the barrier
         }
       }
       __syncthreads();
@@ -685,7 +690,10 @@ __global__ void __launch_bounds__(512) k_tconv_chain(TConvChain c, const TConvAr
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      if (!local) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (!local) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
+      }
       __hip_atomic_store(fl + cg, c.seq0 + (unsigned)l + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the next conv's first weight tile lands while the board's other chunks finish

@@ -82,6 +82,64 @@ def test_batched_games_replay_on_oracle_board(compat):
         assert float(h.final_reward) == (float(gg.winning(st)) if ended else 0.0)
 
 
+FIXED_CASES = [(5, 4, 25, 1.0), (9, 3, 48, 1.0), (9, 2, 32, 0.5)]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("N,G,S,temp", FIXED_CASES, ids=[f"{n}x{n}_g{g}_s{s}_t{t}" for n, g, s, t in FIXED_CASES])
+def test_fixed_compat_games_match_oracle(N, G, S, temp):
+    """compat "fixed" (select_action with the TRUE child visits,
+    self_play.py:376-400 as main.py:666-669 reads them) on whole games, move
+    by move against oracle.selfplay.Agent(compat="fixed"): the same counter
+    streams (SearchHooks: the select draws, and the uniform behind
+    np.random.choice / random.choice) and the Dirichlet sample the device drew
+    at each root (test hook Engine.record_noise: exactly the bench's sampled
+    path).  Identical actions -- visits**(1/T) (T = 0.5: an exact square of
+    integer counts in any pow), numpy's cumulative-sum inverse CDF, and from
+    move 15 on the first-max argmax --, identical policy targets (true visits /
+    sum), root values within 1e-5 (fp32 network)."""
+    import mzgo
+    from oracle.net import OracleNet
+    from oracle.rng import SearchHooks
+    from oracle.selfplay import Agent
+    from oracle.weights import deterministic_state_dict
+    A = N * N + 1
+    seed, C = 4321, 96
+    sp = mzgo.SelfPlay(_net(N, C), G, S, seed=seed, compat="fixed", temperature=temp)
+    drawn = torch.zeros(G, sp.max_moves, A, dtype=torch.float64, device="cuda")
+    sp.engine.record_noise(drawn)
+    try:
+        hists = sp.play()                     # epoch 0: game ids 0 .. G-1 key the streams
+    finally:
+        sp.engine.record_noise(None)
+    drawn = drawn.cpu().numpy()
+    onet = OracleNet(deterministic_state_dict(C, A, 0))
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)                  # batch-1 towers: threads only add overhead
+    sampled = argmaxed = 0
+    try:
+        for g, h in enumerate(hists):
+            st = gg.init_state(N)
+            for mv, (obs, a, pol, v) in enumerate(zip(h.observations, h.actions, h.policies, h.values)):
+                np.testing.assert_array_equal(obs, st)
+                nz = drawn[g, mv]
+                agent = Agent(onet, N, A, S, compat="fixed", noise=lambda p, act, e, nz=nz: (1 - e) * p + e * nz)
+                t = temp if mv < 15 else 0
+                oa, opol, oval = agent.select_action(obs, t, SearchHooks(seed, g, mv))
+                assert a == oa, (g, mv, a, oa)
+                assert pol.tobytes() == np.asarray(opol, np.float64).tobytes(), (g, mv)
+                assert abs(v - oval) < 1e-5, (g, mv, v, oval)
+                sampled += t > 0
+                argmaxed += t == 0
+                st = gg.next_state(st, a)
+            ended = bool(gg.game_ended(st))
+            assert len(h) == N * N or ended
+            assert float(h.final_reward) == (float(gg.winning(st)) if ended else 0.0)
+    finally:
+        torch.set_num_threads(nt)
+    assert sampled > 0 and argmaxed > 0
+
+
 def test_records_pickle_roundtrip(tmp_path):
     import pickle
 

@@ -359,6 +359,50 @@ def test_tower_chain_launch_equals_per_conv_launches(monkeypatch):
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
 
 
+@pytest.mark.timeout(600)
+def test_tower_chain_equals_per_conv_config5(monkeypatch):
+    """The chain's layer hand-offs at BASELINE config 5's own shape: 64 games,
+    19x19, C = 256, 20 blocks (64 x 4 = 256 workgroups, one per CU, every
+    board's 4 cout-chunk workgroups handing 41 layers to each other through
+    the same-XCC path: drained stores + flag, patches read by `sc1` LDS-DMA
+    past the reader's L1).  One move at S = 16 with k_tconv_chain
+    (MZGO_TCONV_CHAIN=1) and with one k_tconv_ks launch per conv (=0) must
+    give byte-identical records, trees of all 64 games and per-node tower
+    outputs (Engine.record_nodes: every node's logits, reward, value)."""
+    import mzgo
+    N, C, blocks, G, S = 19, 256, 20, 64, 16
+    A = N * N + 1
+    net = mzgo.ResMuZeroNet(C, A, blocks).to("cuda").eval()
+    net.load_state_dict(mzgo.deterministic_res_state_dict(C, A, blocks, 0))
+    out = []
+    for chain in ("1", "0"):
+        monkeypatch.setenv("MZGO_TCONV_CHAIN", chain)
+        sp = mzgo.SelfPlay(net, G, S, seed=1234)
+        rec = torch.full((G, S + 1, A + 2), float("nan"), dtype=torch.float32, device="cuda")
+        sp.engine.record_nodes(rec)
+        try:
+            sp.reset(epoch=0)
+            sp.move()
+            torch.cuda.synchronize()
+            recs = [sp.engine.record(g) for g in range(G)]
+            trees = [sp.engine.tree(g) for g in range(G)]
+            nodes = rec.cpu().numpy()
+        finally:
+            sp.engine.record_nodes(None)
+        out.append((recs, trees, nodes))
+    (ra, ta, na), (rb, tb, nb) = out
+    assert np.isfinite(na[:, :S + 1]).all()
+    assert na.tobytes() == nb.tobytes()
+    for a, b in zip(ra, rb):
+        assert a.keys() == b.keys()
+        for k in a:
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    for g, (a, b) in enumerate(zip(ta, tb)):
+        assert int(a["n"]) == S + 1, g
+        for k in a:
+            assert np.asarray(a[k]).tobytes() == np.asarray(b[k]).tobytes(), (g, k)
+
+
 def test_tower_chain_wait_expiry_is_reported(monkeypatch):
     """An expired k_tconv_chain wait (the launch's results are wrong) is
     reported by the API call that made it -- here a single move() -- as
