@@ -87,6 +87,27 @@ def cpu_baseline(N, C, S, budget_s=12.0, blocks=None, threads=1):
                       f"(oracle MCTS + torch-CPU {net_name}; host has {os.cpu_count()} cpus)"}
 
 
+def cpu_share():
+    """(cores, source): the CPU share this process may use for the baseline --
+    the cgroup's CPU quota if one is set, else the per-GPU share the GPU box
+    exports as OMP_NUM_THREADS (16 per GPU; the box's affinity mask and
+    os.cpu_count() show the whole machine), else the affinity mask
+    (scripts/cpu_scaling.py -> profiles/r6_cpu_scaling.json: what the box
+    reports and how the baseline scales past the share)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period))), f"cgroup cpu.max {quota} {period}"
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) <= aff:
+        return int(omp), f"OMP_NUM_THREADS={omp} (the box's per-GPU CPU share; affinity mask {aff} cpus)"
+    return aff, f"affinity mask ({aff} cpus)"
+
+
 def _cpu_worker(a):
     return cpu_baseline(*a)
 
@@ -542,8 +563,8 @@ def main():
                          "games instead of idling while the epoch's slowest games finish (the epoch tail)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
-                    help="oracle processes for cpu_baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="oracle processes for cpu_baseline (default: this host's CPU share, cpu_share())")
     args = ap.parse_args()
     defaults = {2: dict(board_size=9, games=256, sims=200, latent_dim=96, steps=20, warmup=3),
                 5: dict(board_size=19, games=64, sims=1600, latent_dim=256, steps=2, warmup=1)}[args.config]
@@ -551,6 +572,9 @@ def main():
         if getattr(args, k) is None:
             setattr(args, k, v)
 
+    share, share_src = cpu_share()
+    if args.cpu_procs is None:
+        args.cpu_procs = share
     blocks = args.blocks if args.config == 5 else None
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # --gpus N without a launcher: N fresh rank processes (RANK / LOCAL_RANK /
@@ -563,6 +587,7 @@ def main():
             ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget, args.cpu_procs,
                                      blocks)
             ref["measured_in"] = "launcher process, before the ranks started (no GPU work running)"
+            ref["cores_source"] = share_src if args.cpu_procs == share else "--cpu-procs"
             os.environ["MZGO_CPU_BASELINE"] = json.dumps(ref)
         sys.exit(_launch_module().spawn_ranks(
             args.gpus, [sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]]))
@@ -588,6 +613,7 @@ def main():
             # rank 0 in init_process_group meanwhile
             cpu_ref = cpu_baseline_procs(args.board_size, args.latent_dim, args.sims, args.cpu_budget,
                                          args.cpu_procs, blocks)
+            cpu_ref["cores_source"] = share_src if args.cpu_procs == share else "--cpu-procs"
             if world > 1:
                 cpu_ref["measured_in"] = "rank 0, before GPU initialisation (the other ranks waiting)"
     if world > 1:

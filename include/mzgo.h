@@ -117,11 +117,15 @@ int mzgo_search(mzgo_engine* eng, const float* root_obs, const double* noise, in
  * n_nodes; child i32 [n][A]; visits i32 [n]; value_sum f64 [n]; prior f32 [n][A]
  * (row 0 unused); root_prior f64 [A].  Buffers must hold S+1 nodes; NULL skips.
  * After mzgo_search every row is final.  After mzgo_selfplay_move on the
- * reference network (tower = 0), the rows of nodes that no select reached may
- * still hold the child's policy logits (prior) and stale ids (child): both
- * are formed when a select first reaches a node (it has no children before),
- * and the move never reads the others.  Tower engines settle such rows here
- * first (the search API's settle kernel), so their exports are complete. */
+ * reference network (tower = 0), a node that no select reached has NO formed
+ * rows: a batched child's policy head is lazy (never computed), so its prior
+ * row holds whatever an earlier search left there and its child row either
+ * the same stale ids (boards whose tree lives in LDS, 5x5-9x9: the node is
+ * marked in the kernel's LDS bitmask) or the sentinel -3 in entry 0 (HBM
+ * trees, 19x19); the rows are formed when a select first reaches the node
+ * (it has no children before), and the move never reads the others.  Tower
+ * engines settle such rows here first (the search API's settle kernel), so
+ * their exports are complete. */
 int mzgo_tree_export(mzgo_engine* eng, int g, int32_t* n_nodes_host, int32_t* child_host,
                      int32_t* visits_host, double* value_sum_host, float* prior_host,
                      double* root_prior_host, void* stream);
@@ -145,14 +149,19 @@ int mzgo_board_set(mzgo_engine* eng, int g, const int8_t* stones_host, const uin
  * slot.  selfplay_counters (host u64 [8], synchronises; cumulative over the
  * engine's life): [0] simulations run, [1] moves played, [2] games finished,
  * [3] slots still playing now, [4] dynamics 3x3 convs run by searches (one per
- * expansion with direct_dynamics, one per new parent node when factored),
+ * expansion with direct_dynamics, one per new parent node when factored;
+ * tower engines: dynamics towers evaluated, speculative batch entries that
+ * were never used included),
  * [5] of those, parent convs shared with the workgroups of games that had
  * already ended (9x9 whole-game launches: the epoch tail), [6] prior rows
  * formed by searches (a node's child priors + child row written to HBM: every
  * eagerly expanded child, and a lazily expanded one -- the lazy policy head --
  * only when a select first reaches it; 0 on tower engines), [7] self-play
  * game workgroups started (every slot's workgroup of every launch counts one
- * when it begins: mzgo_stream_wait_started's count). */
+ * when it begins: mzgo_stream_wait_started's count), [8] epoch-tail helper
+ * workgroups whose bounded wait for a job expired (they stop helping; records
+ * are unaffected).  counters_host must hold 9 values.  An expired
+ * mzgo_stream_wait_started gate is reported here (MZGO_EHIP, once). */
 int mzgo_selfplay_reset(mzgo_engine* eng, int epoch, void* stream);
 int mzgo_selfplay_move(mzgo_engine* eng, void* stream);
 /* Up to ``moves`` consecutive moves of every unfinished slot in ONE launch
@@ -177,13 +186,16 @@ int mzgo_arena_move(mzgo_engine* eng, mzgo_engine* opponent, void* stream);
 /* ``moves`` arena moves per slot in one launch (as mzgo_selfplay_moves). */
 int mzgo_arena_moves(mzgo_engine* eng, mzgo_engine* opponent, int moves, void* stream);
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
-/* Enqueue on ``stream`` a gate that completes once counter [7] (self-play
- * workgroups started) reaches ``target``: work queued behind it -- a
- * collective -- cannot take a CU before every workgroup of the self-play
- * launch that brings the count to target is resident (a self-play workgroup
- * fills a CU's LDS).  The gate itself is one wave without LDS, so it sits
- * beside them; its wait is bounded (~seconds).  bench.py --gpus N gates each
- * epoch's record gather on the next epoch's launch this way. */
+/* DIAGNOSTIC (scripts/rccl_standin.py; not part of the self-play protocol, and
+ * bench.py does not call it: it gathers every timed epoch's records in ONE
+ * collective after the timed loop).  Enqueue on ``stream`` a gate that
+ * completes once counter [7] (self-play workgroups started) reaches
+ * ``target``: work queued behind it -- a collective -- cannot take a CU before
+ * every workgroup of the self-play launch that brings the count to target is
+ * resident (a self-play workgroup fills a CU's LDS).  The gate itself is one
+ * wave without LDS, so it sits beside them; its wait is bounded (~seconds)
+ * and an expiry is reported by the next mzgo_selfplay_counters call.  Tower
+ * engines: MZGO_EINVAL (they never count started workgroups). */
 int mzgo_stream_wait_started(mzgo_engine* eng, uint64_t target, void* stream);
 /* Tower engines (tower = 1): report (synchronising) and reset the time spent
  * in the dynamics towers since the last call -- one HIP event pair around each

@@ -476,14 +476,14 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   chk(e->alloc(&E.game_len, G));
   chk(e->alloc(&E.final_reward, G));
   chk(e->alloc(&E.status, G));
-  chk(e->alloc(&E.counters, 7));
+  chk(e->alloc(&E.counters, kCounters));
   chk(e->alloc(&e->d_err, 1));
 #ifdef MZGO_STAMPS
   chk(e->alloc(&E.stamps, G * kStampPhases));
   if (E.stamps) (void)hipMemset(E.stamps, 0, G * kStampPhases * 8);
 #endif
   if (rc != MZGO_OK) { delete e; return rc; }
-  if (hipMemset(E.counters, 0, 7 * sizeof(unsigned long long)) != hipSuccess ||
+  if (hipMemset(E.counters, 0, kCounters * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess) {
     delete e;
     return fail(MZGO_EHIP, "hipMemset failed");
@@ -695,15 +695,15 @@ int mzgo_selfplay_reset(mzgo_engine* e, int epoch, void* stream) {
 // job slots zeroed before the launch (batch_expand_shared)
 // CUs of the current device (one self-play workgroup fills a CU's LDS)
 static int device_cus() {
-  static int ncu = -1;
-  if (ncu < 0) {
-    int dev = 0;
-    ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 0;
+  static int ncu[64];                  // per device ordinal (0: not read yet)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (ncu[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    ncu[dev] = n;
   }
-  return ncu;
+  return ncu[dev];
 }
 
 // The epoch tail (whole-game launches): a workgroup whose game has ended
@@ -711,7 +711,11 @@ static int device_cus() {
 // launch is resident at once (one per CU): otherwise ended workgroups would
 // hold CUs that games not yet dispatched are waiting for.  MZGO_TAIL_HELPERS=0
 // turns it off, =2 forces it on past that bound (a test of the kernel's own
-// guards: helpers never join a game whose workgroup has not started).
+// guards: helpers never join a game whose workgroup has not started).  The
+// bound is per launch: engines launched concurrently on several streams (bench.py
+// --refill) share the CUs, so their launches are not all resident even when
+// each fits -- the started guard keeps that correct, but ended workgroups then
+// hold CUs the other engines' games need, and --refill sets MZGO_TAIL_HELPERS=0.
 static bool tail_enabled(int workgroups) {
   const char* v = getenv("MZGO_TAIL_HELPERS");
   const int mode = v ? atoi(v) : 1;
@@ -897,7 +901,7 @@ int mzgo_tower_record_nodes(mzgo_engine* e, float* dst) {
 int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   if (!e || !out) return fail(MZGO_EINVAL, "bad argument");
   hipStream_t s = (hipStream_t)stream;
-  unsigned long long c[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long c[kCounters] = {};
   std::vector<int> st(e->G);
   HIPCHK(hipMemcpyAsync(c, e->E.counters, sizeof c, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(st.data(), e->E.status, e->G * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -906,7 +910,13 @@ int mzgo_selfplay_counters(mzgo_engine* e, uint64_t* out, void* stream) {
   int playing = 0;
   for (int v : st) playing += v == 0;
   out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = (uint64_t)playing; out[4] = c[3]; out[5] = c[4];
-  out[6] = c[5]; out[7] = c[6];
+  out[6] = c[5]; out[7] = c[6]; out[8] = c[7];
+  if (c[8] != 0) {                   // a mzgo_stream_wait_started gate gave up (bounded wait)
+    const unsigned long long zero = 0;
+    HIPCHK(hipMemcpyAsync(e->E.counters + 8, &zero, sizeof zero, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return fail(MZGO_EHIP, "mzgo_stream_wait_started: %llu gate(s) gave up before the target count", c[8]);
+  }
   return MZGO_OK;
 }
 
@@ -949,21 +959,28 @@ int mzgo_debug_stamps(mzgo_engine* e, unsigned long long* host) {
 }
 #endif
 
-// A gate for a collective (mzgo_stream_wait_started): one wave, no LDS and a
-// handful of registers, so it sits beside a self-play workgroup on any CU;
-// it returns once *count >= target (or after a bounded ~seconds wait)
-__global__ void __launch_bounds__(64) k_wait_count(const unsigned long long* count, unsigned long long target) {
+// A gate for a collective (mzgo_stream_wait_started, a diagnostic entry
+// point): one wave, no LDS and a handful of registers, so it sits beside a
+// self-play workgroup on any CU; it returns once *count >= target, or after
+// a bounded ~seconds wait, which it records in *expired (reported by the next
+// mzgo_selfplay_counters call)
+__global__ void __launch_bounds__(64) k_wait_count(const unsigned long long* count, unsigned long long target,
+                                                  unsigned long long* expired) {
   if (threadIdx.x != 0) return;
   for (long long spins = 0; spins < (1ll << 26); ++spins) {
     if (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
     __builtin_amdgcn_s_sleep(16);
   }
+  atomicAdd(expired, 1ull);
 }
 
 int mzgo_stream_wait_started(mzgo_engine* e, uint64_t target, void* stream) {
   if (!e || e->C == 0) return fail(MZGO_EINVAL, "bad argument");
+  // tower engines run a move as many small launches and never count
+  // workgroups_started: the gate would only time out
+  if (e->tower) return fail(MZGO_EINVAL, "mzgo_stream_wait_started: not for tower engines");
   hipLaunchKernelGGL(k_wait_count, dim3(1), dim3(64), 0, (hipStream_t)stream, e->E.counters + 6,
-                     (unsigned long long)target);
+                     (unsigned long long)target, e->E.counters + 8);
   HIPCHK(hipGetLastError());
   return MZGO_OK;
 }

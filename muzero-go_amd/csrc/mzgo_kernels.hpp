@@ -78,6 +78,8 @@ __device__ __forceinline__ NetParams launder_params(const NetParams& n) {
   return r;
 }
 
+constexpr int kCounters = 9;     // EngineArrays::counters
+
 // Per-slot device state of an engine (sizes fixed at engine creation).
 struct EngineArrays {
   int S;                 // simulations per move this engine was sized for
@@ -109,10 +111,13 @@ struct EngineArrays {
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
   unsigned char* jobs;   // [G][job_bytes(A)] batch-expansion jobs shared with helper workgroups
-  unsigned long long* counters;  // [7] 0: simulations run, 1: moves played, 2: games finished,
-                                 //     3: dynamics convs run (factored: one per new parent),
+  unsigned long long* counters;  // [kCounters] 0: simulations run, 1: moves played, 2: games finished,
+                                 //     3: dynamics convs run (factored: one per new parent; tower
+                                 //     engines: towers evaluated, speculative ones included),
                                  //     4: of those, tail conv jobs (conv_tail), 5: prior rows formed,
-                                 //     6: game workgroups started (k_selfplay_move)
+                                 //     6: game workgroups started (k_selfplay_move), 7: tail helpers
+                                 //     whose bounded wait for a job expired (tail_help), 8: expired
+                                 //     mzgo_stream_wait_started gates (reported, then cleared)
   unsigned long long* stamps;    // [G][kStampPhases] phase cycles (MZGO_STAMPS builds only)
 };
 
@@ -820,6 +825,7 @@ __device__ __forceinline__ void tail_help(Smem<G>& sm, const NetParams& np_a, co
           int expired = 0;
           if (s == last || s == 0) {                   // (bounded wait: leave, and exit -- no re-registering)
             __hip_atomic_fetch_sub(J.nhelp(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(&E.counters[7], 1ull);           // (counted: bench lines report expiries)
             s = kJobExit;
             expired = 1;
           }

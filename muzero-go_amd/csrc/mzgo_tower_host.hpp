@@ -170,6 +170,10 @@ struct TowerHost {
       if ((e = hipEventRecord(c.done, s)) != hipSuccess) return e;
       c.host = L;
     }
+    // a slot found by its contents may have been uploaded on another stream:
+    // this launch reads it only after that upload
+    if (slot->stream && slot->stream != s && slot->done && (e = hipStreamWaitEvent(s, slot->done, 0)) != hipSuccess)
+      return e;
     const TConvArgs* dev = slot->dev;
     slot->stream = s;
     // MZGO_TCONV_CHAIN_SPIN: the waits' bound (test hook: a negative bound

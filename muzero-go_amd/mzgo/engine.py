@@ -241,17 +241,20 @@ class Engine:
         return ms.value, n.value
 
     def counters(self):
-        out = np.zeros(8, np.uint64)
+        out = np.zeros(9, np.uint64)
         check(lib.mzgo_selfplay_counters(self._h, ptr(out), stream_of(self.device)))
         return dict(simulations=int(out[0]), moves=int(out[1]), games_finished=int(out[2]),
                     playing=int(out[3]), dynamics_convs=int(out[4]), tail_convs=int(out[5]),
-                    prior_rows=int(out[6]), workgroups_started=int(out[7]))
+                    prior_rows=int(out[6]), workgroups_started=int(out[7]), tail_wait_expiries=int(out[8]))
 
     def wait_started(self, target, stream=None):
-        """Enqueue on ``stream`` (default: the current one) a gate that
-        completes once ``counters()['workgroups_started'] >= target``: a
-        collective queued behind it cannot displace a self-play workgroup of
-        the launch that brings the count there (mzgo_stream_wait_started)."""
+        """Diagnostic (scripts/rccl_standin.py; bench.py does not use it):
+        enqueue on ``stream`` (default: the current one) a gate that completes
+        once ``counters()['workgroups_started'] >= target``: a collective
+        queued behind it cannot displace a self-play workgroup of the launch
+        that brings the count there (mzgo_stream_wait_started; reference
+        network engines only; a gate that gives up is reported by the next
+        counters() call)."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         check(lib.mzgo_stream_wait_started(self._h, int(target), ctypes.c_void_p(s.cuda_stream)))
 

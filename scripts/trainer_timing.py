@@ -1,8 +1,9 @@
 """The batched trainer step (main.py:381-501's losses, mzgo.trainer
 mode="batched") at main.py's configuration -- 6x6 board, latent_dim 128,
 batch 128 trajectories x unroll 10 -- with the unroll's forward and every 3x3
-conv backward on the HIP kernels (csrc/mzgo_train.hip; hip_forward=True, the
-default on the GPU) against torch's ops (MIOpen convs; hip_forward=False).
+conv backward on the HIP kernels (csrc/mzgo_train.hip; hip_forward=True)
+against torch's ops (MIOpen convs; hip_forward=False, MuZeroTrainer's default
+since round 5, when MIOpen measured faster).
 Same trajectories, same start indices, alternating, same process.
 
 Usage (GPU box): python scripts/trainer_timing.py [tag] -> one JSON line

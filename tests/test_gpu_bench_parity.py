@@ -295,7 +295,7 @@ def test_tail_helpers_do_not_change_records(epoch, monkeypatch):
         out[on] = (recs, arrays, {k: c1[k] - c0[k] for k in c1 if k != "playing"})
     (ra, aa, ca), (rb, ab, cb) = out["1"], out["0"]
     assert ca["tail_convs"] > 0 and cb["tail_convs"] == 0, (ca, cb)
-    assert {k: v for k, v in ca.items() if k != "tail_convs"} == {k: v for k, v in cb.items() if k != "tail_convs"}
+    assert {k: v for k, v in ca.items() if k not in ("tail_convs", "tail_wait_expiries")} == {k: v for k, v in cb.items() if k not in ("tail_convs", "tail_wait_expiries")}
     for k in aa:
         np.testing.assert_array_equal(aa[k].view(np.uint8), ab[k].view(np.uint8), err_msg=k)
 
@@ -327,7 +327,7 @@ def test_tail_helpers_games_above_cu_count(monkeypatch):
     assert out["1"][1]["games_finished"] == G
     for mode in ("1", "2"):
         a, c = out[mode]
-        assert {k: v for k, v in c.items() if k != "tail_convs"} == \
-            {k: v for k, v in out["0"][1].items() if k != "tail_convs"}
+        assert {k: v for k, v in c.items() if k not in ("tail_convs", "tail_wait_expiries")} == \
+            {k: v for k, v in out["0"][1].items() if k not in ("tail_convs", "tail_wait_expiries")}
         for k in a:
             np.testing.assert_array_equal(a[k].view(np.uint8), out["0"][0][k].view(np.uint8), err_msg=f"{mode} {k}")
