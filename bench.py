@@ -267,38 +267,41 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
 PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
-def tower_roofline(N, C, blocks, G, sims, tower_ms, towers, towers_run):
-    """Config 5's dominant kernel: the tower conv (one 3x3 conv of every active
-    leaf, bf16 MFMA).  Algorithmic FLOPs per launch = boards x 2 x N^2 x 9 x C^2
-    (the conv as the network defines it; the kernel also multiplies the
-    16-row tiles' pad rows: executed = boards x 2 x 16*ceil(N^2/16) x 9 x C^2),
-    over the average launch duration = the timed towers' event spans / the
-    2*blocks+1 launches of a tower (so the inter-launch gaps are included)."""
+def tower_roofline(N, C, blocks, G, sims, tower_ms, board_towers, evaluated):
+    """Config 5's dominant kernel: the tower conv (one 3x3 conv of a batch of
+    boards, bf16 MFMA).  Algorithmic FLOPs per board and conv = 2 x N^2 x 9 x
+    C^2 (the conv as the network defines it; the kernel also multiplies the
+    16-row tiles' pad rows: executed x 16*ceil(N^2/16) / N^2).  The timed
+    towers (HIP events on the launch stream around each batched step's tower,
+    or every 16th one-leaf step's) covered ``board_towers`` boards x L convs in
+    ``tower_ms``, so achieved = board_towers x L x FLOP per board-conv / time
+    (inter-launch gaps included).  ``evaluated`` = towers run (the engine's
+    counter, speculative entries that were dropped included) over ``sims``."""
     L = 2 * blocks + 1
-    avg_launch_s = tower_ms / 1e3 / max(towers, 1) / L   # (towers: the timed ones, every 16th)
-    boards = sims / max(towers_run, 1)                   # leaves evaluated per tower (terminal leaves skip)
-    alg = boards * 2 * N * N * 9 * C * C
-    exe = boards * 2 * 16 * ((N * N + 15) // 16) * 9 * C * C
-    ach = alg / avg_launch_s / 1e12
-    # one k_tconv_chain launch per tower (all L convs) unless MZGO_TCONV_CHAIN=0
-    chain = os.environ.get("MZGO_TCONV_CHAIN") != "0" and G * (C // 64) <= 256
+    per_bt_s = tower_ms / 1e3 / max(board_towers, 1)      # one board through the whole tower
+    alg = 2 * N * N * 9 * C * C
+    exe = 2 * 16 * ((N * N + 15) // 16) * 9 * C * C
+    ach = alg * L / per_bt_s / 1e12
+    batched = os.environ.get("MZGO_TOWER_BATCH", "0") != "0"
+    chain = not batched and os.environ.get("MZGO_TCONV_CHAIN") != "0" and G * (C // 64) <= 256
     kname = "k_tconv_chain" if chain else "k_tconv_ks"
     out = {"bound": "mfma", "kernel": f"{kname}<{N}>", "achieved": ach, "peak": PEAK_BF16_MFMA_TFLOPS,
            "unit": "TFLOP/s", "frac": ach / PEAK_BF16_MFMA_TFLOPS, "traffic": None,
-           "avg_launch_ms": avg_launch_s * 1e3, "launches_per_simulation": L, "boards_per_launch": boards,
-           "flops_per_launch": alg, "executed_flops_per_launch": exe,
-           "mfma_executed_tflops": exe / avg_launch_s / 1e12,
-           "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board) / average time per conv "
-                   "(HIP events around every 16th simulation's tower / its L convs, gaps included; "
-                   "k_tconv_chain runs a tower's L convs in one launch, so its per-launch counters are / L)"}
-    if chain:
-        out["convs_per_launch"] = L
+           "us_per_board_conv": per_bt_s / L * 1e6, "us_per_64_board_conv": per_bt_s / L * 64e6,
+           "board_towers_timed": board_towers, "convs_per_tower": L,
+           "flops_per_board_conv": alg, "executed_flops_per_board_conv": exe,
+           "mfma_executed_tflops": exe * L / per_bt_s / 1e12,
+           "towers_per_simulation": evaluated / max(sims, 1),
+           "steps": "batched (k_tbatch: root children + speculative leaf batches)" if batched else "one leaf per game",
+           "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board and conv) x boards x L / the timed towers' "
+                   "HIP-event spans (gaps included)"}
     path = os.path.join(ROOT, "profiles", "latest_tower_pmc.json")
     if os.path.exists(path):
         p = json.load(open(path))
         if p.get("workload") == f"{N}x{N}/C{C}/B{blocks}/G{G}" and ("chain" in p.get("kernel", "")) == chain:
             per = L if chain else 1                     # (the chain's counters cover L convs)
             out["traffic"] = p.get("hbm_bytes_per_launch") / per if p.get("hbm_bytes_per_launch") else None
+            out["traffic_per"] = "launch of the PMC workload"
             out["pmc_source"] = f"profiles/{p['tag']}_pmc.json"
             out["pmc"] = p.get("derived")
             clk = (p.get("derived") or {}).get("in_kernel_clock_GHz")
@@ -374,6 +377,8 @@ def tower_main(args, world, rank, local, cpu_ref):
     c1 = eng.counters()
     sims = c1["simulations"] - c0["simulations"]
     moves = c1["moves"] - c0["moves"]
+    evaluated = c1["dynamics_convs"] - c0["dynamics_convs"]      # tower engines: towers evaluated
+    sims_local = sims
     if world > 1:
         t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64,
                          device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
@@ -384,9 +389,10 @@ def tower_main(args, world, rank, local, cpu_ref):
     if rank == 0:
         workload = f"{N}x{N} Go self-play, {B}-block residual nets (C={C}), {G} parallel games/GPU, {S} sims/move"
         mps = args.moves_per_step
-        roof = tower_roofline(N, C, B, G, sims / world, tower_ms, towers, S * args.steps * mps)
-        # the conv kernel's share of the step: launches x average launch / wall time
-        roof["share_of_step"] = roof["avg_launch_ms"] / 1e3 * (2 * B + 1) * S * args.steps * mps / dt
+        roof = tower_roofline(N, C, B, G, sims_local, tower_ms, towers, evaluated)
+        # the towers' share of the step: timed tower spans / wall time (batched
+        # steps time every tower; one-leaf steps every 16th, scaled up)
+        roof["share_of_step"] = (tower_ms / 1e3 * (1.0 if os.environ.get("MZGO_TOWER_BATCH", "0") != "0" else 16.0)) / dt
         out = {
             "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {B}-block residual "
                       f"nets, {S} sims/move (BASELINE config 5)",

@@ -725,6 +725,19 @@ struct TowerArrays {
   HeadScalars hs;
   const float* headw;    // [3][C]: reward_conv, value_conv, policy_conv
   float* node_out;       // test hook (mzgo_tower_record_nodes): [G][S+1][A+2] logits, reward, value; or null
+  // batched simulation steps (k_tbatch / k_tboards / k_tbexpand): each game's
+  // pending batch -- the leaf, its first node id, and per entry the action and
+  // the tower's reward and value once evaluated
+  int bq_cap;            // entries per game
+  int* bq_n;             // [G] entries of the pending batch (0: none)
+  int* bq_leaf;          // [G][bq_cap] the node entry i expands
+  int* bq_nid0;          // [G] node id of entry 0 (entry i's latent: pool slot g*(S+1) + nid0 + i)
+  int* bq_act;           // [G][bq_cap]
+  float* bq_rv;          // [G][bq_cap][2] reward, value
+  int* nbg;              // [G] boards this step
+  // this step's boards, all games (k_tboards): leaf slot, output slot, action, game, entry
+  int* b_in; int* b_out; int* b_act; int* b_game; int* b_ent;
+  int* b_total;          // [1] boards this step
 };
 
 template <class G>
@@ -883,7 +896,7 @@ __global__ void __launch_bounds__(64) k_troot(TowerArrays T, SearchParams sp, En
   root_priors<G>(t, TV, sp, nz, T.key[g]);
   TreeAcc<G, false> acc(TV, t);
   tree_reset_root<G>(acc);
-  if (threadIdx.x == 0) { E.nodes[g] = 1; T.simc[g] = 0; }
+  if (threadIdx.x == 0) { E.nodes[g] = 1; T.simc[g] = 0; T.bq_n[g] = 0; }
 }
 
 // select_leaf for one simulation of every game -> the conv jobs
@@ -957,7 +970,321 @@ __global__ void __launch_bounds__(64) k_texpand(TowerArrays T, SearchParams sp, 
   if (threadIdx.x == (a & 63)) acc.set_child(leaf, a, nid);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   backup<G>(acc, depth, nid, (double)r + sp.discount * (double)v, sp.variant == 0);
-  if (threadIdx.x == 0) { E.nodes[g] = nid + 1; T.simc[g] += 1; }
+  if (threadIdx.x == 0) {
+    E.nodes[g] = nid + 1;
+    T.simc[g] += 1;
+    atomicAdd(&E.counters[3], 1ull);      // towers evaluated
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Batched simulation steps.  The tree stays the sequential one because
+// every simulation still runs the real select on the real tree: k_tbatch
+// commits a pending entry (leaf L_i, action a_i) only when the select asks
+// for exactly that expansion as the next node id, and otherwise drops the
+// batch's remaining entries and starts a new batch at the select's own leaf.
+// A batch is a prediction of the next simulations' expansions:
+//  * the root's children: while the root has unexpanded eligible children
+//    every simulation picks one by its draw alone (random.choice,
+//    self_play.py:283-287), no value involved -- so the first min(#eligible,
+//    S) simulations are ONE batch per game, always committed whole;
+//  * after that, each simulation's PUCT walk (:296-330) goes to the root
+//    child of highest score, whose score then drops (its visit count rises:
+//    the exploration term shrinks), so the next simulations are predicted by
+//    replaying the root's choice with virtual visits -- q held at its current
+//    mean, n and N raised by each predicted visit: entry k >= 1 is the root
+//    child c that choice takes for simulation sim + k and the pick sim + k
+//    would make there, the randbelow(draw(sim + k), n)-th of c's unexpanded
+//    eligible children less those this batch already gave to c.  The batch
+//    stops at a child with no unexpanded child left (the walk would go
+//    deeper) or at cap_spec entries.
+// Entry i's latent is written straight into node nid0 + i's pool slot, its
+// logits into that node's prior row (the lazy kRawRow form of k_texpand): a
+// committed entry is in place; a dropped one's slot and rows belong to the
+// node that later takes its id, which overwrites them before any select can
+// reach it.
+// ---------------------------------------------------------------------------
+constexpr int kSpecMax = 128;   // entries of a speculative (non-root) batch
+
+template <int N>
+__global__ void __launch_bounds__(64) k_tbatch(TowerArrays T, SearchParams sp, EngineArrays E, int cap_root,
+                                               int cap_spec) {
+  typedef TGeo<N> G;
+  const int g = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (!T.playing[g]) {
+    if (lane == 0) { T.nbg[g] = 0; T.bq_n[g] = 0; }
+    return;
+  }
+  __shared__ TreeLds<G> t;
+  __shared__ int sl_leaf[kSpecMax], sl_act[kSpecMax];   // the batch being formed (LDS copy)
+  tload_mask<G>(t, T, g);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  TreeAcc<G, false> acc(TV, t);
+  const uint64_t key = T.key[g];
+  const int S = sp.num_simulations;
+  int sim = T.simc[g], nodes = E.nodes[g];
+  const int bn = T.bq_n[g], bnid0 = T.bq_nid0[g];
+  int* const bact = T.bq_act + (size_t)g * T.bq_cap;
+  int* const bleaf = T.bq_leaf + (size_t)g * T.bq_cap;
+  const float* const brv = T.bq_rv + (size_t)g * T.bq_cap * 2;
+  int next = 0, B = 0;
+  while (sim < S) {
+    const int a = select_leaf<G>(t, acc, sp, key, sim);
+    if (a < 0) {
+      // self_play.py: a terminal leaf backs up 0 (:188-191); main.py: nothing (:296)
+      if (a == -1) backup<G>(acc, t.depth, -1, 0.0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ++sim;
+      continue;
+    }
+    if (next < bn && nodes == bnid0 + next && t.leaf == __builtin_amdgcn_readfirstlane(bleaf[next]) &&
+        a == __builtin_amdgcn_readfirstlane(bact[next])) {
+      // the expansion this simulation asks for was evaluated: k_texpand's commit
+      const float r = brv[2 * next], v = brv[2 * next + 1];
+      if (lane == 0) acc.init(nodes);
+      if (lane == (a & 63)) acc.set_child(t.leaf, a, nodes);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      backup<G>(acc, t.depth, nodes, (double)r + sp.discount * (double)v, sp.variant == 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ++nodes;
+      ++sim;
+      ++next;
+      continue;
+    }
+    const int room = S - sim;
+    if (t.leaf == 0) {
+      // the root's unexpanded children, in the order the draws take them
+      B = t.nunexp < room ? t.nunexp : room;
+      B = B < cap_root ? B : cap_root;
+      PickSeq<G> ps(t.umask, t.nunexp, B, key, sim);
+      for (int i = 0; i < B; ++i) {
+        const int ai = ps.pick(i);
+        if (lane == 0) { bact[i] = ai; bleaf[i] = 0; }
+      }
+    } else {
+      // this simulation's expansion, then the next ones predicted by
+      // replaying the root's PUCT choice with virtual visits
+      if (lane == 0) { bact[0] = a; bleaf[0] = t.leaf; sl_leaf[0] = t.leaf; sl_act[0] = a; }
+      B = 1;
+      int lim = cap_spec < room ? cap_spec : room;
+      lim = lim < kSpecMax ? lim : kSpecMax;
+      if (lim > 1) {
+        // the root children's stats, updated by each predicted visit: n (and
+        // the root's N) + 1, and the child's q moved toward the mean q of the
+        // root's children (the visit's value is unknown; a child chosen for
+        // its high q tends to fall back: on the oracle's config-5 trees this
+        // predicted 15 of the next 16 choices, against 11 with q held and 14
+        // with the static ranking); puct_pick's formula on the
+        // virtual statistics
+        double P[G::AP], q[G::AP];
+        int ch[G::AP], n[G::AP];
+        uint64_t elig[G::AP];
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j) {
+          const int aa = lane + 64 * j;
+          P[j] = aa < G::A ? TV.root_prior[aa] : 0.0;
+          ch[j] = aa < G::A ? TV.child[aa] : -1;
+        }
+        double qsum = 0.0;
+        int ne = 0;
+#pragma unroll
+        for (int j = 0; j < G::AP; ++j) {
+          const bool e = P[j] > 0.0 && ch[j] >= 0;
+          elig[j] = __ballot(e);
+          n[j] = e ? TV.visits[ch[j]] : 0;
+          const double w = e ? TV.wsum[ch[j]] : 0.0;
+          q[j] = e && n[j] > 0 ? ddiv(w, (double)n[j]) : 0.0;
+          if (e) { qsum += q[j]; ++ne; }
+        }
+        qsum = wave_sum(qsum);
+        ne = (int)wave_sum((double)ne);
+        const double qmean = ne > 0 ? qsum / ne : 0.0;
+        int nvis = TV.visits[0];
+        auto virtual_visit = [&](int act) {
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j)
+            if (lane + 64 * j == act) { q[j] = (q[j] * n[j] + qmean) / (double)(n[j] + 1); n[j] += 1; }
+          ++nvis;
+        };
+        virtual_visit(t.ract);                      // this simulation's own visit
+        while (B < lim) {
+          double lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j)
+            if ((elig[j] >> lane) & 1ull) { lo = fmin_(lo, q[j]); hi = fmax_(hi, q[j]); }
+          wave_minmax(lo, hi);
+          const double sq = dsqrt((double)(sp.variant == 1 ? nvis + 1 : (nvis > 1 ? nvis : 1)));
+          double best = -INFINITY;
+          double sc[G::AP];
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            sc[j] = -INFINITY;
+            if ((elig[j] >> lane) & 1ull) {
+              const double qn = hi > lo ? ddiv(q[j] - lo, hi - lo) : q[j];
+              sc[j] = qn + ddiv((sp.c_puct * P[j]) * sq, (double)(1 + n[j]));
+            }
+            best = sc[j] > best ? sc[j] : best;
+          }
+          best = wave_max(best);
+          if (!(best > -INFINITY)) break;
+          int ca = -1, c = -1;
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            const uint64_t hit = __ballot(sc[j] == best);
+            if (ca < 0 && hit) {
+              const int l = __ffsll((long long)hit) - 1;
+              ca = 64 * j + l;
+              c = __builtin_amdgcn_readlane(ch[j], l);
+            }
+          }
+          // c's unexpanded eligible children (prior > 0, child -1: select's
+          // test), less the ones this batch already gave to c.  A row still
+          // in the lazy kRawRow form is settled here, exactly as select_leaf
+          // settles it on its first arrival (the priors depend on the logits
+          // and the root mask alone, so settling early changes nothing)
+          int* crow = TV.child + (size_t)c * G::A;
+          float* prow = TV.prior + (size_t)c * G::A;
+          float pr[G::AP];
+          int cr[G::AP];
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            const int aa = lane + 64 * j;
+            pr[j] = aa < G::A ? prow[aa] : 0.f;
+            cr[j] = aa < G::A ? crow[aa] : 0;
+          }
+          if (__builtin_amdgcn_readfirstlane(cr[0]) == kRawRow) {
+            float qq[G::AP];
+            child_prior_regs<G>(t, pr, qq, sp.variant, t.fbuf, t.dbuf);
+#pragma unroll
+            for (int j = 0; j < G::AP; ++j) {
+              const int aa = lane + 64 * j;
+              if (aa < G::A) { prow[aa] = qq[j]; crow[aa] = -1; }
+              pr[j] = qq[j];
+              cr[j] = -1;
+            }
+          }
+          bool taken[G::AP];
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) taken[j] = false;
+          for (int e = 0; e < B; ++e)
+            if (sl_leaf[e] == c) {
+              const int ae = sl_act[e];
+#pragma unroll
+              for (int j = 0; j < G::AP; ++j) taken[j] |= lane + 64 * j == ae;
+            }
+          uint64_t un[G::AP];
+          int nun = 0;
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            const int aa = lane + 64 * j;
+            un[j] = __ballot(aa < G::A && pr[j] > 0.f && cr[j] < 0 && !taken[j]);
+            nun += __popcll(un[j]);
+          }
+          if (nun == 0) break;                     // c is fully expanded: the walk would go deeper
+          uint32_t k = randbelow(draw(key, TAG_SELECT, (uint64_t)(sim + B)), (uint32_t)nun);
+          int pick = -1;
+#pragma unroll
+          for (int j = 0; j < G::AP; ++j) {
+            const uint32_t cnt = __popcll(un[j]);
+            if (pick < 0 && k < cnt) pick = 64 * j + kth_set_bit(un[j], k);
+            else if (pick < 0) k -= cnt;
+          }
+          if (lane == 0) { bact[B] = pick; bleaf[B] = c; sl_leaf[B] = c; sl_act[B] = pick; }
+          wave_lds_sync();
+          ++B;
+          virtual_visit(ca);
+        }
+      }
+    }
+    if (lane == 0) T.bq_nid0[g] = nodes;
+    break;
+  }
+  if (lane == 0) {
+    T.bq_n[g] = B;
+    T.nbg[g] = B;
+    T.simc[g] = sim;
+    E.nodes[g] = nodes;
+  }
+}
+
+// This step's boards of all games, in game order (one block): board
+// off[g] + i = game g's entry i; the count to b_total, and to counters[3]
+// (towers evaluated).
+template <int N>
+__global__ void __launch_bounds__(256) k_tboards(TowerArrays T, EngineArrays E, int G) {
+  __shared__ int part[256];
+  const int tid = threadIdx.x;
+  // per-thread sums of a contiguous range of games, then an exclusive scan
+  const int per = (G + 255) / 256;
+  int s = 0;
+  for (int k = 0; k < per; ++k) {
+    const int g = tid * per + k;
+    if (g < G) s += T.nbg[g];
+  }
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int i = 0; i < 256; ++i) { const int v = part[i]; part[i] = acc; acc += v; }
+    *T.b_total = acc;
+    if (acc > 0) atomicAdd(&E.counters[3], (unsigned long long)acc);
+  }
+  __syncthreads();
+  int o = part[tid];
+  for (int k = 0; k < per; ++k) {
+    const int g = tid * per + k;
+    if (g >= G) break;
+    const int nb = T.nbg[g];
+    const int base = g * (E.S + 1);
+    const int nid0 = nb > 0 ? T.bq_nid0[g] : 0;
+    for (int i = 0; i < nb; ++i) {
+      const int b = o + i;
+      T.b_in[b] = base + T.bq_leaf[(size_t)g * T.bq_cap + i];
+      T.b_out[b] = base + nid0 + i;
+      T.b_act[b] = T.bq_act[(size_t)g * T.bq_cap + i];
+      T.b_game[b] = g;
+      T.b_ent[b] = i;
+    }
+    o += nb;
+  }
+}
+
+// heads of this step's boards (one wave per board): the entry's reward and
+// value for the commit, its logits into node nid0 + i's prior row (kRawRow:
+// select_leaf forms the priors on its first arrival, as after k_texpand)
+template <int N>
+__global__ void __launch_bounds__(64) k_tbexpand(TowerArrays T, SearchParams sp, EngineArrays E) {
+  typedef TGeo<N> G;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  __shared__ float hp[3 * G::CS];
+  __shared__ float hsc[64];
+  stage_head_scalars(T.hs, hsc);
+  tsum_heads<G>(T, b, hp);
+  const int g = T.b_game[b], i = T.b_ent[b];
+  const int nid = T.b_out[b] - g * (E.S + 1);
+  float r, v;
+  heads_value<G, 1>(hp, true, hsc, r, v);
+  float x[G::AP];
+  logits_regs<G, 1>(hp, true, hsc, x);
+  const TreeView TV = TreeViewOf<G>::make(E, g);
+  float* prow = TV.prior + (size_t)nid * G::A;
+#pragma unroll
+  for (int j = 0; j < G::AP; ++j)
+    if (lane + 64 * j < G::A) prow[lane + 64 * j] = x[j];
+  if (lane == 0) {
+    TV.child[(size_t)nid * G::A] = kRawRow;
+    T.bq_rv[((size_t)g * T.bq_cap + i) * 2] = r;
+    T.bq_rv[((size_t)g * T.bq_cap + i) * 2 + 1] = v;
+  }
+  if (T.node_out) {                       // (test hook) the node as the tower evaluated it
+    float* o = T.node_out + ((size_t)g * (E.S + 1) + nid) * (G::A + 2);
+#pragma unroll
+    for (int j = 0; j < G::AP; ++j)
+      if (lane + 64 * j < G::A) o[lane + 64 * j] = x[j];
+    if (lane == 0) { o[G::A] = r; o[G::A + 1] = v; }
+  }
 }
 
 // action choice, record, board step (self_play.py:465-507), as k_selfplay_move's tail
@@ -1009,7 +1336,6 @@ __global__ void __launch_bounds__(64) k_tchoose(TowerArrays T, SearchParams sp, 
     E.rec_reward[rec] = w;
     atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);
     atomicAdd(&E.counters[1], 1ull);
-    atomicAdd(&E.counters[3], (unsigned long long)sp.num_simulations);   // a tower per simulation
     if (st != BOARD_OK) {
       E.status[g] = 16 + st;
     } else if (m.done || m.moves >= E.max_moves) {

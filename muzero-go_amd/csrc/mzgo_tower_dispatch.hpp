@@ -22,6 +22,10 @@ struct TowerSet {
                      long long game_stride, int per_move, int G, hipStream_t);
   hipError_t (*select)(const TowerArrays&, const SearchParams&, const EngineArrays&, int G, hipStream_t);
   hipError_t (*expand)(const TowerArrays&, const SearchParams&, const EngineArrays&, int G, hipStream_t);
+  // batched steps: k_tbatch (+ k_tboards: the step's board list and count), k_tbexpand
+  hipError_t (*batch)(const TowerArrays&, const SearchParams&, const EngineArrays&, int G, int cap_root,
+                      int cap_spec, hipStream_t);
+  hipError_t (*bexpand)(const TowerArrays&, const SearchParams&, const EngineArrays&, int nb, hipStream_t);
   hipError_t (*choose)(const TowerArrays&, const SearchParams&, const PlayParams&, const EngineArrays&, int G,
                        hipStream_t);
   hipError_t (*search_out)(const TowerArrays&, const SearchParams&, const EngineArrays&, int G, int* visits,
@@ -72,6 +76,19 @@ struct TLaunch {
     hipLaunchKernelGGL((k_texpand<N>), dim3(G), dim3(64), 0, s, T, sp, E);
     return hipGetLastError();
   }
+  static hipError_t batch(const TowerArrays& T, const SearchParams& sp, const EngineArrays& E, int G, int cap_root,
+                          int cap_spec, hipStream_t s) {
+    hipLaunchKernelGGL((k_tbatch<N>), dim3(G), dim3(64), 0, s, T, sp, E, cap_root, cap_spec);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_tboards<N>), dim3(1), dim3(256), 0, s, T, E, G);
+    return hipGetLastError();
+  }
+  static hipError_t bexpand(const TowerArrays& T, const SearchParams& sp, const EngineArrays& E, int nb,
+                            hipStream_t s) {
+    hipLaunchKernelGGL((k_tbexpand<N>), dim3(nb), dim3(64), 0, s, T, sp, E);
+    return hipGetLastError();
+  }
   static hipError_t choose(const TowerArrays& T, const SearchParams& sp, const PlayParams& pp,
                            const EngineArrays& E, int G, hipStream_t s) {
     hipLaunchKernelGGL((k_tchoose<N>), dim3(G), dim3(64), 0, s, T, sp, pp, E);
@@ -96,8 +113,8 @@ struct TLaunch {
     return hipGetLastError();
   }
   static TowerSet table() {
-    return TowerSet{N, &conv, &chain, &obs, &obs_search, &root, &select, &expand, &choose, &search_out, &tin, &tout,
-                    &theads};
+    return TowerSet{N, &conv, &chain, &obs, &obs_search, &root, &select, &expand, &batch, &bexpand, &choose,
+                    &search_out, &tin, &tout, &theads};
   }
 };
 

@@ -65,15 +65,30 @@ struct TowerHost {
   HeadScalars hs{};
 
   // optional timing of the dynamics towers (bench.py --config 5): one event
-  // pair around every kTimeEvery-th simulation step's tower, on the launch
-  // stream (an event record between two kernels costs a ~3 us dispatch gap:
-  // around every tower that was 0.5 % of the simulation time)
+  // pair around every kTimeEvery-th simulation step's tower (one leaf per
+  // game), or around every batched step's tower, on the launch stream (an
+  // event record between two kernels costs a ~3 us dispatch gap: around every
+  // one-leaf tower that was 0.5 % of the simulation time)
   static constexpr int kTimeEvery = 16;
   bool timing = false;
   std::vector<hipEvent_t> evs;
+  std::vector<long long> ev_boards;   // boards of the tower behind each event pair
   size_t ev_used = 0;
-  long long towers_timed = 0;
+  long long towers_timed = 0;         // board-towers: boards summed over the timed towers
   double tower_ms = 0.0;
+
+  // batched simulation steps (k_tbatch, mzgo_tower.hpp; MZGO_TOWER_BATCH=1):
+  // per game up to bq_cap pending entries (the root's children: min(A, S); a
+  // non-root leaf's speculative batch: MZGO_TOWER_SPEC, default kSpecCap), so
+  // up to G * bq_cap boards per step.  The default keeps one leaf per game
+  // per step (k_tselect / k_texpand).  kSpecCap = 1: on the
+  // config-5 network the next simulations' root children are predicted for
+  // ~7-8 of 16, so speculative entries would cost more
+  // towers than larger batches save with the current conv kernel.
+  static constexpr int kSpecCap = 1;
+  int bq_cap = 0, maxb = 0;
+  int* h_total = nullptr;             // pinned: the step's board count
+  long long steps_run = 0;
 
   long long slot() const { return (long long)CC * P * 64; }
 
@@ -214,14 +229,17 @@ struct TowerHost {
     cerr = nullptr;
   }
 
-  hipError_t mark(hipStream_t s) {
+  // boards: of the tower that starts at this mark (its end mark passes 0)
+  hipError_t mark(hipStream_t s, long long boards = 0) {
     if (!timing) return hipSuccess;
     if (ev_used == evs.size()) {
       hipEvent_t e;
       hipError_t r = hipEventCreate(&e);
       if (r != hipSuccess) return r;
       evs.push_back(e);
+      ev_boards.push_back(0);
     }
+    ev_boards[ev_used] = boards;
     return hipEventRecord(evs[ev_used++], s);
   }
   // sum the recorded spans (synchronises) and recycle the events
@@ -232,7 +250,7 @@ struct TowerHost {
       float ms = 0.f;
       if ((r = hipEventElapsedTime(&ms, evs[i], evs[i + 1])) != hipSuccess) return r;
       tower_ms += ms;
-      towers_timed += 1;
+      towers_timed += ev_boards[i];
     }
     ev_used = 0;
     return hipSuccess;
@@ -406,13 +424,50 @@ struct TowerHost {
     return ts->root(TA, sp, E, noise, nstride, per_move, G, s);
   }
 
-  // S simulations: select (all games) -> dynamics tower (all leaves) -> expand + backup
+  // S simulations of every game
   hipError_t simulations(const SearchParams& sp, const EngineArrays& E, hipStream_t s) {
+    // batched steps only on request (MZGO_TOWER_BATCH=1, read per call):
+    // measured on config 5 they do not pay with this conv kernel (DESIGN.md
+    // §4b: 64.0 k sims/s with the root batch and one leaf per step after it,
+    // 64.7 k one leaf per step throughout, 50.6 k / 38.1 k with 4 / 8
+    // speculative entries, same call)
+    const char* env = getenv("MZGO_TOWER_BATCH");
+    if (!env || atoi(env) == 0) return simulations_one_leaf(sp, E, s);
+    int spec = kSpecCap;
+    if (const char* v = getenv("MZGO_TOWER_SPEC")) spec = atoi(v);
+    spec = spec < 1 ? 1 : (spec > bq_cap ? bq_cap : spec);
+    hipError_t e;
+    // one step: commit what the previous step evaluated, form the next batch
+    // per game (k_tbatch), the step's board list (k_tboards); then the tower
+    // over all of them and their heads.  The host reads the board count (the
+    // grid of the next launches): one small synchronising copy per step.
+    for (;;) {
+      if ((e = ts->batch(TA, sp, E, G, bq_cap, spec, s)) != hipSuccess) return e;
+      if ((e = hipMemcpyAsync(h_total, TA.b_total, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+      const int nb = *h_total;
+      if (nb <= 0) break;
+      if (nb > maxb) return hipErrorInvalidValue;          // (cannot happen: bq_cap entries per game)
+      ++steps_run;
+      if ((e = mark(s, nb)) != hipSuccess) return e;
+      if ((e = tower(dyn, TA.pool, TA.b_in, slot(), TA.pool, TA.b_out, slot(), TA.b_act, nullptr, nb, t0, t1,
+                     TA.hpart, s)) != hipSuccess)
+        return e;
+      if ((e = mark(s)) != hipSuccess) return e;
+      if ((e = ts->bexpand(TA, sp, E, nb, s)) != hipSuccess) return e;
+    }
+    if (timing) return harvest();
+    return hipSuccess;
+  }
+
+  // one leaf per game per step: select (all games) -> dynamics tower (all
+  // leaves) -> expand + backup, S times
+  hipError_t simulations_one_leaf(const SearchParams& sp, const EngineArrays& E, hipStream_t s) {
     hipError_t e;
     for (int i = 0; i < S; ++i) {
       const bool tm = i % kTimeEvery == 0;
       if ((e = ts->select(TA, sp, E, G, s)) != hipSuccess) return e;
-      if (tm && (e = mark(s)) != hipSuccess) return e;
+      if (tm && (e = mark(s, G)) != hipSuccess) return e;
       if ((e = tower(dyn, TA.pool, TA.in_idx, slot(), TA.pool, TA.out_idx, slot(), TA.act, TA.evalact, G, t0, t1,
                      TA.hpart, s)) != hipSuccess)
         return e;

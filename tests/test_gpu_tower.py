@@ -339,6 +339,7 @@ def test_tower_chain_launch_equals_per_conv_launches(monkeypatch):
     import mzgo
     N, C, blocks, G, S = 9, 128, 2, 8, 24
     net = _nets(N, C, blocks, seed=5)[0]
+    monkeypatch.setenv("MZGO_TOWER_BATCH", "0")   # one leaf per game per step: 8-board towers, always chained
     out = []
     for chain in ("1", "0"):
         monkeypatch.setenv("MZGO_TCONV_CHAIN", chain)
@@ -374,6 +375,7 @@ def test_tower_chain_equals_per_conv_config5(monkeypatch):
     A = N * N + 1
     net = mzgo.ResMuZeroNet(C, A, blocks).to("cuda").eval()
     net.load_state_dict(mzgo.deterministic_res_state_dict(C, A, blocks, 0))
+    monkeypatch.setenv("MZGO_TOWER_BATCH", "0")   # one leaf per game per step: every tower a 64-board chain
     out = []
     for chain in ("1", "0"):
         monkeypatch.setenv("MZGO_TCONV_CHAIN", chain)
@@ -403,6 +405,64 @@ def test_tower_chain_equals_per_conv_config5(monkeypatch):
             assert np.asarray(a[k]).tobytes() == np.asarray(b[k]).tobytes(), (g, k)
 
 
+BATCH_CASES = [(5, 64, 1, 8, 25, 4, "8"), (9, 64, 1, 6, 120, 2, "32"), (19, 64, 2, 4, 400, 1, "32"),
+               (19, 64, 1, 4, 300, 1, "3")]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("N,C,blocks,G,S,moves,spec", BATCH_CASES,
+                         ids=[f"{c[0]}x{c[0]}_g{c[3]}_s{c[4]}_spec{c[6]}" for c in BATCH_CASES])
+def test_tower_batched_steps_equal_one_leaf_steps(N, C, blocks, G, S, moves, spec, monkeypatch):
+    """Batched simulation steps (k_tbatch: the root's children as one batch
+    per game, speculative batches of a leaf's next picks, every entry
+    committed only when the sequential select asks for exactly it) against one
+    leaf per game per step (MZGO_TOWER_BATCH=0, k_tselect / k_texpand): the
+    same trees node for node (ids, visits, f64 value sums, priors), the same
+    per-node tower outputs (Engine.record_nodes) and byte-identical records.
+    Only the number of towers evaluated differs (dropped speculative
+    entries), never below one per expansion."""
+    import mzgo
+    A = N * N + 1
+    net = _nets(N, C, blocks, seed=2)[0]
+    monkeypatch.setenv("MZGO_TOWER_SPEC", spec)
+    out = []
+    for batched in ("1", "0"):
+        monkeypatch.setenv("MZGO_TOWER_BATCH", batched)
+        sp = mzgo.SelfPlay(net, G, S, seed=31)
+        eng = sp.engine
+        rec = torch.full((G, S + 1, A + 2), float("nan"), dtype=torch.float32, device="cuda")
+        eng.record_nodes(rec)
+        try:
+            c0 = eng.counters()
+            sp.reset(epoch=1)
+            trees = []
+            for _ in range(moves):
+                sp.move()
+                torch.cuda.synchronize()
+                trees.append([eng.tree(g) for g in range(G)])
+            c1 = eng.counters()
+            recs = [eng.record(g) for g in range(G)]
+            nodes = rec.cpu().numpy()
+        finally:
+            eng.record_nodes(None)
+        out.append((recs, trees, nodes, {k: c1[k] - c0[k] for k in ("simulations", "moves", "dynamics_convs")}))
+    (ra, ta, na, ca), (rb, tb, nb, cb) = out
+    assert ca["simulations"] == cb["simulations"] and ca["moves"] == cb["moves"]
+    assert ca["dynamics_convs"] >= cb["dynamics_convs"] > 0, (ca, cb)
+    for a, b in zip(ra, rb):
+        for k in a:
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    for mv, (tma, tmb) in enumerate(zip(ta, tb)):
+        for g, (a, b) in enumerate(zip(tma, tmb)):
+            assert int(a["n"]) == int(b["n"]), (mv, g)
+            for k in a:
+                assert np.asarray(a[k]).tobytes() == np.asarray(b[k]).tobytes(), (mv, g, k)
+    # the last move's nodes (record_nodes rows are node ids of the current search)
+    for g in range(G):
+        n = int(ta[-1][g]["n"])
+        assert na[g, :n].tobytes() == nb[g, :n].tobytes(), g
+
+
 def test_tower_chain_wait_expiry_is_reported(monkeypatch):
     """An expired k_tconv_chain wait (the launch's results are wrong) is
     reported by the API call that made it -- here a single move() -- as
@@ -414,10 +474,12 @@ def test_tower_chain_wait_expiry_is_reported(monkeypatch):
     net = _nets(N, C, blocks, seed=3)[0]
     sp = mzgo.SelfPlay(net, G, S, seed=5)
     sp.reset()
+    monkeypatch.setenv("MZGO_TOWER_BATCH", "0")
     monkeypatch.setenv("MZGO_TCONV_CHAIN_SPIN", "-1")
     with pytest.raises(mzgo.MzgoError, match="k_tconv_chain"):
         sp.move()
     monkeypatch.delenv("MZGO_TCONV_CHAIN_SPIN")
+    monkeypatch.delenv("MZGO_TOWER_BATCH")
     sp.engine.counters()
     sp.reset()
     sp.move()
@@ -448,9 +510,13 @@ class _ReplayNet:
                 torch.from_numpy(o[:self.A].copy()).reshape(1, self.A))
 
 
+C5_REPLAY_CASES = [c + ("0",) for c in C5_TREE_CASES] + [(400, 2, 128, "16"), (0, 0, 64, "16")]
+
+
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("moves,seed,S", C5_TREE_CASES, ids=[f"m{m}_s{s}_S{S}" for m, s, S in C5_TREE_CASES])
-def test_tower_config5_tree_exact_replay(moves, seed, S):
+@pytest.mark.parametrize("moves,seed,S,spec", C5_REPLAY_CASES,
+                         ids=[f"m{m}_s{s}_S{S}" + (f"_batched{b}" if b != "0" else "") for m, s, S, b in C5_REPLAY_CASES])
+def test_tower_config5_tree_exact_replay(moves, seed, S, spec, monkeypatch):
     """Config 5's real network (19x19, C=256, 20 blocks): the oracle's
     MCTS.run (self_play.py:148-237 restated) driven by the device's OWN tower
     outputs per node (logits, reward, value as k_texpand / k_troot produced
@@ -458,7 +524,12 @@ def test_tower_config5_tree_exact_replay(moves, seed, S):
     the device's tree exactly: identical root-child visits, every node's
     visit count and value sum (the same f64 additions in the same order).
     Any difference is a search defect, not bf16 rounding -- the bounded test
-    above compares against a separately computed (bf16-emulating) network."""
+    above compares against a separately computed (bf16-emulating) network.
+    spec != "0": the batched steps (MZGO_TOWER_BATCH=1: the root's children
+    as one batch, then speculative batches of up to ``spec`` entries)."""
+    if spec != "0":
+        monkeypatch.setenv("MZGO_TOWER_BATCH", "1")
+        monkeypatch.setenv("MZGO_TOWER_SPEC", spec)
     import mzgo
     from oracle.mcts import MCTS as OracleMCTS
     from oracle.positions import random_position
