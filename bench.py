@@ -292,6 +292,8 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, board_towers, evaluated):
            "flops_per_board_conv": alg, "executed_flops_per_board_conv": exe,
            "mfma_executed_tflops": exe * L / per_bt_s / 1e12,
            "towers_per_simulation": evaluated / max(sims, 1),
+           # one leaf per game per step: a conv launch (a chain launch's layer) covers G boards
+           "avg_launch_ms": per_bt_s / L * G * 1e3, "boards_per_launch": G, "flops_per_launch": alg * G,
            "steps": "batched (k_tbatch: root children + speculative leaf batches)" if batched else "one leaf per game",
            "what": "algorithmic conv FLOPs (2 N^2 9 C^2 per board and conv) x boards x L / the timed towers' "
                    "HIP-event spans (gaps included)"}
@@ -301,7 +303,7 @@ def tower_roofline(N, C, blocks, G, sims, tower_ms, board_towers, evaluated):
         if p.get("workload") == f"{N}x{N}/C{C}/B{blocks}/G{G}" and ("chain" in p.get("kernel", "")) == chain:
             per = L if chain else 1                     # (the chain's counters cover L convs)
             out["traffic"] = p.get("hbm_bytes_per_launch") / per if p.get("hbm_bytes_per_launch") else None
-            out["traffic_per"] = "launch of the PMC workload"
+            out["traffic_per"] = "conv launch (a chain launch's counters / its L convs)"
             out["pmc_source"] = f"profiles/{p['tag']}_pmc.json"
             out["pmc"] = p.get("derived")
             clk = (p.get("derived") or {}).get("in_kernel_clock_GHz")

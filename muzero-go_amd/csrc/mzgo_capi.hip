@@ -232,6 +232,7 @@ struct mzgo_engine {
                       (void*)tower->s1, (void*)tower->shp, (void*)tower->sact})
         if (p) (void)hipFree(p);
       if (tower->h_total) (void)hipHostFree(tower->h_total);
+      tower->free_batch();
       delete tower;
     }
     for (void* p : allocs) (void)hipFree(p);
@@ -422,36 +423,28 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     TowerArrays& T = t->TA;
     T.C = C; T.co_chunks = C / 64;
     const size_t slot = (size_t)t->slot();
-    // batched simulation steps: up to min(A, S) pending entries per game (the
-    // root's children), so up to G x that many boards per step
+    // batched simulation steps (MZGO_TOWER_BATCH=1): up to min(A, S) pending
+    // entries per game (the root's children), so up to G x that many boards
+    // per step; their buffers are allocated on first use (ensure_batch)
     t->bq_cap = (int)std::min<size_t>(A, n1 - 1);
     t->maxb = (int)(G * (size_t)t->bq_cap);
-    const size_t MB = (size_t)t->maxb;
     T.bq_cap = t->bq_cap;
     // node latents (bf16, zero borders: the conv's padding is never written);
-    // the tower's two scratch activations per board of a step
+    // the tower's two scratch activations per board of a one-leaf step
     chk(e->alloc(&T.pool, G * n1 * slot));
-    chk(e->alloc(&t->t0, MB * slot));
-    chk(e->alloc(&t->t1, MB * slot));
+    chk(e->alloc(&t->t0, G * slot));
+    chk(e->alloc(&t->t1, G * slot));
     chk(e->alloc(&T.rep_in, G * (size_t)t->P * 64));
     if (rc == MZGO_OK) {
-      for (auto pr : {std::make_pair((void*)T.pool, G * n1 * slot), std::make_pair((void*)t->t0, MB * slot),
-                      std::make_pair((void*)t->t1, MB * slot), std::make_pair((void*)T.rep_in, G * (size_t)t->P * 64)})
+      for (auto pr : {std::make_pair((void*)T.pool, G * n1 * slot), std::make_pair((void*)t->t0, G * slot),
+                      std::make_pair((void*)t->t1, G * slot), std::make_pair((void*)T.rep_in, G * (size_t)t->P * 64)})
         if (hipMemset(pr.first, 0, pr.second * sizeof(bf16)) != hipSuccess) chk(fail(MZGO_EHIP, "hipMemset(tower) failed"));
     }
     T.slot = (long long)slot;
-    chk(e->alloc(&T.hpart, MB * (size_t)t->CC * 3 * e->CS));
+    chk(e->alloc(&T.hpart, G * (size_t)t->CC * 3 * e->CS));
     chk(e->alloc(&T.bq_n, G));
-    chk(e->alloc(&T.bq_leaf, MB));
     chk(e->alloc(&T.bq_nid0, G));
-    chk(e->alloc(&T.bq_act, MB));
-    chk(e->alloc(&T.bq_rv, 2 * MB));
     chk(e->alloc(&T.nbg, G));
-    chk(e->alloc(&T.b_in, MB));
-    chk(e->alloc(&T.b_out, MB));
-    chk(e->alloc(&T.b_act, MB));
-    chk(e->alloc(&T.b_game, MB));
-    chk(e->alloc(&T.b_ent, MB));
     chk(e->alloc(&T.b_total, 1));
     if (rc == MZGO_OK && (hipMemset(T.bq_n, 0, G * sizeof(int)) != hipSuccess ||
                           hipHostMalloc(&t->h_total, sizeof(int), hipHostMallocDefault) != hipSuccess))

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "mzgo_tower_dispatch.hpp"
@@ -89,6 +90,38 @@ struct TowerHost {
   int bq_cap = 0, maxb = 0;
   int* h_total = nullptr;             // pinned: the step's board count
   long long steps_run = 0;
+  // the batched steps' buffers (maxb boards), allocated on first use: the
+  // tower's two scratch activations and head partials per board, the
+  // pending entries and the step's board list
+  bf16* bt0 = nullptr; bf16* bt1 = nullptr; float* bhp = nullptr;
+  std::vector<void*> batch_allocs;
+  hipError_t ensure_batch(hipStream_t s) {
+    if (bt0) return hipSuccess;
+    hipError_t e;
+    const size_t MB = (size_t)maxb;
+    auto get = [&](auto** p, size_t n) {
+      void* v = nullptr;
+      hipError_t r = hipMalloc(&v, n * sizeof(**p) + 256);
+      if (r == hipSuccess) { batch_allocs.push_back(v); *p = reinterpret_cast<std::remove_pointer_t<decltype(p)>>(v); }
+      return r;
+    };
+    if ((e = get(&bt0, MB * slot())) != hipSuccess || (e = get(&bt1, MB * slot())) != hipSuccess ||
+        (e = get(&bhp, MB * CC * 3 * CS)) != hipSuccess || (e = get(&TA.bq_leaf, MB)) != hipSuccess ||
+        (e = get(&TA.bq_act, MB)) != hipSuccess || (e = get(&TA.bq_rv, 2 * MB)) != hipSuccess ||
+        (e = get(&TA.b_in, MB)) != hipSuccess || (e = get(&TA.b_out, MB)) != hipSuccess ||
+        (e = get(&TA.b_act, MB)) != hipSuccess || (e = get(&TA.b_game, MB)) != hipSuccess ||
+        (e = get(&TA.b_ent, MB)) != hipSuccess)
+      return e;
+    // zero borders of the scratch activations (the conv's padding is never written)
+    if ((e = hipMemsetAsync(bt0, 0, MB * slot() * sizeof(bf16), s)) != hipSuccess) return e;
+    return hipMemsetAsync(bt1, 0, MB * slot() * sizeof(bf16), s);
+  }
+  void free_batch() {
+    for (void* p : batch_allocs) (void)hipFree(p);
+    batch_allocs.clear();
+    bt0 = bt1 = nullptr;
+    bhp = nullptr;
+  }
 
   long long slot() const { return (long long)CC * P * 64; }
 
@@ -437,12 +470,15 @@ struct TowerHost {
     if (const char* v = getenv("MZGO_TOWER_SPEC")) spec = atoi(v);
     spec = spec < 1 ? 1 : (spec > bq_cap ? bq_cap : spec);
     hipError_t e;
+    if ((e = ensure_batch(s)) != hipSuccess) return e;
+    TowerArrays TB = TA;                                  // the step kernels' view: per-board head partials
+    TB.hpart = bhp;
     // one step: commit what the previous step evaluated, form the next batch
     // per game (k_tbatch), the step's board list (k_tboards); then the tower
     // over all of them and their heads.  The host reads the board count (the
     // grid of the next launches): one small synchronising copy per step.
     for (;;) {
-      if ((e = ts->batch(TA, sp, E, G, bq_cap, spec, s)) != hipSuccess) return e;
+      if ((e = ts->batch(TB, sp, E, G, bq_cap, spec, s)) != hipSuccess) return e;
       if ((e = hipMemcpyAsync(h_total, TA.b_total, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
       if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
       const int nb = *h_total;
@@ -450,11 +486,11 @@ struct TowerHost {
       if (nb > maxb) return hipErrorInvalidValue;          // (cannot happen: bq_cap entries per game)
       ++steps_run;
       if ((e = mark(s, nb)) != hipSuccess) return e;
-      if ((e = tower(dyn, TA.pool, TA.b_in, slot(), TA.pool, TA.b_out, slot(), TA.b_act, nullptr, nb, t0, t1,
-                     TA.hpart, s)) != hipSuccess)
+      if ((e = tower(dyn, TA.pool, TA.b_in, slot(), TA.pool, TA.b_out, slot(), TA.b_act, nullptr, nb, bt0, bt1,
+                     bhp, s)) != hipSuccess)
         return e;
       if ((e = mark(s)) != hipSuccess) return e;
-      if ((e = ts->bexpand(TA, sp, E, nb, s)) != hipSuccess) return e;
+      if ((e = ts->bexpand(TB, sp, E, nb, s)) != hipSuccess) return e;
     }
     if (timing) return harvest();
     return hipSuccess;

@@ -13,8 +13,8 @@ declare -A A=(
   [9_400]="--sims 400 --steps 8 --warmup 1 --no-cpu-baseline"
   [refill2]="--refill 2 --steps 20 --warmup 2 --no-cpu-baseline"
   [19_64]="--board-size 19 --games 64 --sims 800 --steps 2 --warmup 1 --no-cpu-baseline"
-  [c5]="--config 5 --no-cpu-baseline"
-  [c5mid]="--config 5 --start-move 100 --no-cpu-baseline"
+  [c5]="--config 5 --cpu-budget 20"
+  [c5mid]="--config 5 --start-move 100 --cpu-budget 20"
 )
 for l in ${LINES:-bench 9_400 refill2 19_64 c5}; do
   timeout -k 10 ${LIMIT:-420} python bench.py ${A[$l]} > gpurun_out/${TAG}_$l.json 2> gpurun_out/${TAG}_$l.err || { tail -5 gpurun_out/${TAG}_$l.err; exit 1; }
