@@ -87,7 +87,7 @@ def cpu_baseline(N, C, S, budget_s=12.0, blocks=None, threads=1):
                       f"(oracle MCTS + torch-CPU {net_name}; host has {os.cpu_count()} cpus)"}
 
 
-def cpu_share():
+def cpu_share(cgroup_cpu_max="/sys/fs/cgroup/cpu.max"):
     """(cores, source): the CPU share this process may use for the baseline --
     the cgroup's CPU quota if one is set, else the per-GPU share the GPU box
     exports as OMP_NUM_THREADS (16 per GPU; the box's affinity mask and
@@ -95,7 +95,7 @@ def cpu_share():
     (scripts/cpu_scaling.py -> profiles/r6_cpu_scaling.json: what the box
     reports and how the baseline scales past the share)."""
     try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
+        with open(cgroup_cpu_max) as f:
             quota, period = f.read().split()[:2]
         if quota != "max":
             return max(1, int(int(quota) // int(period))), f"cgroup cpu.max {quota} {period}"

@@ -1,0 +1,46 @@
+"""bench.py's host-side logic (no GPU): the CPU share the cpu_baseline leg
+uses, and config 5's roofline arithmetic."""
+import os
+
+import pytest
+
+import bench
+
+
+def test_cpu_share_prefers_the_cgroup_quota(tmp_path, monkeypatch):
+    f = tmp_path / "cpu.max"
+    f.write_text("1600000 100000\n")
+    monkeypatch.setenv("OMP_NUM_THREADS", "4")
+    assert bench.cpu_share(str(f)) == (16, "cgroup cpu.max 1600000 100000")
+
+
+def test_cpu_share_without_quota(tmp_path, monkeypatch):
+    f = tmp_path / "cpu.max"
+    f.write_text("max 100000\n")
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    n, src = bench.cpu_share(str(f))
+    assert n == 1 and src.startswith("OMP_NUM_THREADS=1")
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_share(str(tmp_path / "absent")) == (aff, f"affinity mask ({aff} cpus)")
+    # an OMP_NUM_THREADS beyond the affinity mask is not a share
+    monkeypatch.setenv("OMP_NUM_THREADS", str(aff + 1))
+    assert bench.cpu_share(str(f))[0] == aff
+
+
+@pytest.mark.parametrize("batched", ["0", "1"])
+def test_tower_roofline_arithmetic(batched, monkeypatch):
+    """achieved = boards x L x 2 N^2 9 C^2 / time; per-launch values for G boards."""
+    monkeypatch.setenv("MZGO_TOWER_BATCH", batched)
+    N, C, B, G = 19, 256, 20, 64
+    L = 2 * B + 1
+    board_towers = 6400                      # e.g. 100 timed one-leaf towers of 64 boards
+    ms = 6400 * L * 0.35e-3                  # 0.35 us per board-conv
+    r = bench.tower_roofline(N, C, B, G, 102400, ms, board_towers, 110000)
+    flop = 2 * N * N * 9 * C * C
+    assert r["flops_per_board_conv"] == flop
+    assert abs(r["achieved"] - flop / 0.35e-6 / 1e12) < 1e-6 * r["achieved"]
+    assert abs(r["avg_launch_ms"] - 0.35e-3 * G) < 1e-12
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert abs(r["towers_per_simulation"] - 110000 / 102400) < 1e-12
+    assert r["kernel"] == ("k_tconv_chain<19>" if batched == "0" else "k_tconv_ks<19>")
