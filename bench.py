@@ -4,10 +4,15 @@ BASELINE.json's metric on configs[1]: 256 parallel self-play games per GPU,
 200 simulations per move, the reference network (latent_dim 96) with
 deterministic random-init weights, fp32.  One *step* = one whole self-play
 epoch: all 256 games from the empty board until
-every one has ended -- one launch of the fused k_selfplay_move kernel that
-plays every game's moves back to back (each move: observation record,
-representation + root priors, 200 simulations of select / dynamics +
-prediction / expand / backup, action choice, board step).
+every one has ended.  Under compat "reference" (the bench's protocol, SURVEY
+§0.6: the action is a uniform draw over the legal moves, never read from the
+search) an epoch is the move-parallel pair: k_selfplay_move with the searches
+left out records and steps every game's boards, then k_search_queue runs
+every recorded move's search (representation + root priors, 200 simulations
+of select / dynamics + prediction / expand / backup, the root value) from one
+queue on one workgroup per CU.  MZGO_MOVE_PARALLEL=0 times the
+game-per-workgroup launch instead (one fused k_selfplay_move launch playing
+each game's moves back to back on its CU); the records are byte-identical.
 
 Multi-GPU, one process per GPU: ``bench.py --gpus N`` starts the N rank
 processes itself (or runs under torch.distributed.run with --nproc-per-node
@@ -145,7 +150,7 @@ PEAK_FP32_MFMA_TFLOPS = 157.3
 CUS, PEAK_CLK_GHZ = 256, 2.4
 
 
-def pmc_summary(workload, dynamics, moves_per_launch, n_gpus=1):
+def pmc_summary(workload, dynamics, moves_per_launch, n_gpus=1, kernel="k_selfplay_move"):
     """Per-launch PMC means of k_selfplay_move from rocprofv3 passes of this
     same bench command (scripts/pmc.sh -> profiles/<tag>_pmc.json);
     only a profile of the same workload, launch structure and GPU count
@@ -155,7 +160,8 @@ def pmc_summary(workload, dynamics, moves_per_launch, n_gpus=1):
             sorted(glob.glob(os.path.join(ROOT, "profiles", "latest_pmc_*.json"))):
         p = json.load(open(path))
         if (p.get("workload") == workload and p.get("dynamics") == dynamics
-                and p.get("moves_per_launch", 1) == moves_per_launch and p.get("n_gpus", 1) == n_gpus):
+                and p.get("moves_per_launch", 1) == moves_per_launch and p.get("n_gpus", 1) == n_gpus
+                and kernel in p.get("kernel", "k_selfplay_move")):
             return p
     return None
 
@@ -189,8 +195,12 @@ def phases_summary(workload, moves_per_launch):
     return out
 
 
-def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch, n_gpus=1):
-    """Roofline of the dominant kernel, k_selfplay_move, per launch.
+def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launch, n_gpus=1,
+             kernel="k_selfplay_move"):
+    """Roofline of the dominant kernel, per launch: k_selfplay_move (the
+    game-per-workgroup launch) or, in the move-parallel epoch, k_search_queue
+    (every search of the launch; the boards launch before it records and
+    steps the boards and is timed beside it).
 
     Executed MFMA work: the dynamics convs the searches ran (Winograd GEMMs at
     9x9 / 19x19) + the representation per move.  HBM: the factored algorithm's
@@ -229,7 +239,7 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
                 "what": "algorithmic HBM bytes of the factored search (E[a] table and weights L2-resident, "
                         "not charged; a parent's Y read from the LDS copy still charged)"},
     }
-    pmc = pmc_summary(workload, dynamics, moves_per_launch, n_gpus)
+    pmc = pmc_summary(workload, dynamics, moves_per_launch, n_gpus, kernel)
     traffic = None
     if pmc is not None:
         c = pmc["counters"]
@@ -254,7 +264,7 @@ def roofline(N, C, S, G, counts, avg_kern_s, dynamics, workload, moves_per_launc
         units["clock_GHz"] = clk
     bound = max((k for k in ("mfma", "hbm", "valu", "lds") if k in units), key=lambda k: units[k]["frac"])
     u = units[bound]
-    return {"bound": bound, "kernel": "k_selfplay_move", "achieved": u["achieved"], "peak": u["peak"],
+    return {"bound": bound, "kernel": kernel, "achieved": u["achieved"], "peak": u["peak"],
             "unit": u["unit"], "frac": u["frac"], "traffic": traffic,
             "avg_launch_ms": avg_kern_s * 1e3, "sims_per_launch": sims_l,
             "dynamics_convs_per_move": convs_l / max(moves_l, 1e-9),
@@ -442,6 +452,9 @@ def refill_main(args, net, world, rank, local, cpu_ref):
     # epoch would start on: refill and tail helpers exclude each other
     # (same-call A/B: 106.2 M with them off, 95.6 M on)
     os.environ["MZGO_TAIL_HELPERS"] = "0"
+    # refill is the game-per-workgroup launch's answer to the epoch tail (the
+    # move-parallel epoch is the other): its epochs are k_selfplay_move
+    os.environ["MZGO_MOVE_PARALLEL"] = "0"
     sps = [mzgo.SelfPlay(net, G, S, seed=1234, game_base=(rank * R + r) * G, dynamics=args.dynamics)
            for r in range(R)]
     M = sps[0].max_moves
@@ -703,6 +716,7 @@ def main():
         staged = torch.empty(args.steps * per_epoch, dtype=torch.uint8, device=f"cuda:{local}")
         torch.cuda.synchronize()
 
+    eng.launch_timing(True)        # move-parallel epochs: HIP events around both launches
     t0 = time.perf_counter()
     for i in range(args.steps):
         one_epoch(ev[i])
@@ -719,11 +733,19 @@ def main():
     c1 = eng.counters()
     sims = c1["simulations"] - c0["simulations"]
     moves = c1["moves"] - c0["moves"]
-    # k_selfplay_move launch durations (HIP events on the launch stream), all
-    # launches of every timed epoch
+    # launch durations (HIP events on the launch stream), all launches of every
+    # timed epoch: k_selfplay_move, or in the move-parallel epoch (compat
+    # "reference") the boards launch + k_search_queue, whose own
+    # durations the engine's events give
     kern_ms = [a.elapsed_time(b) for e in ev for a, b in e]
+    boards_ms, queue_ms = eng.launch_timing(False)
     launches = len(kern_ms)
-    avg_kern_s = sum(kern_ms) / launches / 1e3
+    kernel = "k_search_queue" if queue_ms else "k_selfplay_move"
+    if queue_ms:
+        assert len(queue_ms) == launches, (len(queue_ms), launches)
+        avg_kern_s = sum(queue_ms) / launches / 1e3
+    else:
+        avg_kern_s = sum(kern_ms) / launches / 1e3
 
     if world > 1:
         t = torch.tensor([dt, float(sims), float(moves)], dtype=torch.float64,
@@ -738,7 +760,11 @@ def main():
         counts = dict(launches=launches, sims=sims / world, moves=moves / world,
                       convs=(c1["dynamics_convs"] - c0["dynamics_convs"]),
                       rows=(c1["prior_rows"] - c0["prior_rows"]))
-        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload, args.moves_per_launch, world)
+        roof = roofline(N, C, S, G, counts, avg_kern_s, args.dynamics, workload, args.moves_per_launch, world,
+                        kernel)
+        if queue_ms:
+            roof["boards_launch_ms"] = sum(boards_ms) / launches
+            roof["epoch_launches_ms"] = sum(kern_ms) / launches
         out = {
             "metric": f"MCTS simulations/sec (whole node) + self-play moves/sec, {N}x{N} Go, {S} sims/move",
             "value": sims / dt,
@@ -758,7 +784,10 @@ def main():
                                                      f"of up to {per} moves)",
                        "board_size": N, "latent_dim": C, "games_per_gpu": G, "sims_per_move": S,
                        "parallelism": f"game-sharded x{world}", "compat": "reference",
-                       "dynamics": args.dynamics},
+                       "dynamics": args.dynamics,
+                       "schedule": ("move-parallel: boards launch + k_search_queue (every move's search from "
+                                    "one queue, one workgroup per CU)") if queue_ms else
+                                   "game-per-workgroup k_selfplay_move"},
             "roofline": roof,
         }
         if world > 1:
@@ -769,7 +798,9 @@ def main():
                                          "one gather of all of them at the end of the timed loop (inside it): no "
                                          "collective kernel shares the chip with an epoch"}
         # (the stamps build is profiled on one GPU: phase shares only on 1-GPU lines)
-        ph = phases_summary(workload, args.moves_per_launch) if args.dynamics == "factored" and world == 1 else None
+        # (the stamps build profiles the game-per-workgroup launch: MZGO_MOVE_PARALLEL=0 lines only)
+        ph = phases_summary(workload, args.moves_per_launch) if (args.dynamics == "factored" and world == 1
+                                                                 and not queue_ms) else None
         if ph is not None:
             out["phases"] = ph
         if cpu_ref is not None:

@@ -186,6 +186,23 @@ int mzgo_arena_move(mzgo_engine* eng, mzgo_engine* opponent, void* stream);
 /* ``moves`` arena moves per slot in one launch (as mzgo_selfplay_moves). */
 int mzgo_arena_moves(mzgo_engine* eng, mzgo_engine* opponent, int moves, void* stream);
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
+
+/* Move-parallel epoch (no reference counterpart; the schedule, not the
+ * protocol): a multi-move mzgo_selfplay_moves under compat "reference" on
+ * 5x5-9x9 boards runs as two launches -- k_selfplay_move with the searches
+ * left out (observation, action, policy target, board step and reward of
+ * every move: under compat "reference" the action never reads the search)
+ * and k_search_queue, which runs every recorded move's search (root value)
+ * from one work queue on one workgroup per CU.  The records are byte-identical
+ * to the game-per-workgroup launch (MZGO_MOVE_PARALLEL=0 in the environment
+ * keeps that launch); the trees left in the slots are then those of whatever
+ * searches ran last in each queue slot, not one per game.
+ * mzgo_selfplay_set_timing(eng, 1) records HIP events around both launches
+ * of every such call (0 stops and discards); mzgo_selfplay_launch_times
+ * synchronises on them, writes up to ``cap`` (boards, queue) durations in
+ * ms, stores the number recorded in *n_host and clears them. */
+int mzgo_selfplay_set_timing(mzgo_engine* eng, int on);
+int mzgo_selfplay_launch_times(mzgo_engine* eng, float* boards_ms, float* queue_ms, int cap, int* n_host);
 /* DIAGNOSTIC (scripts/rccl_standin.py; not part of the self-play protocol, and
  * bench.py does not call it: it gathers every timed epoch's records in ONE
  * collective after the timed loop).  Enqueue on ``stream`` a gate that

@@ -2,6 +2,7 @@
 // memory, weight packing and dispatch to the per-(N, C) kernel tables.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -193,10 +194,24 @@ std::vector<float> action_taps(const float* W, const float* emb, int C, int A) {
 
 }  // namespace
 
+// CUs of the current device (one self-play workgroup fills a CU's LDS)
+static int device_cus() {
+  static int ncu[64];                  // per device ordinal (0: not read yet)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (ncu[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    ncu[dev] = n;
+  }
+  return ncu[dev];
+}
+
 struct mzgo_engine {
   mzgo_config cfg;
   const KernelSet* ks = nullptr;
   int N = 0, C = 0, A = 0, CELLS = 0, CS = 0, G = 0, S = 0, M = 0;
+  int TS = 0;                   // search-tree slots: G, or the CU count when larger (move-parallel epoch)
   std::map<std::string, std::vector<float>> sd;  // host copies of the state_dict
   std::vector<Spec> spec;
   bool dirty = true;
@@ -208,6 +223,11 @@ struct mzgo_engine {
   float* d_scr = nullptr;      // initial_inference scratch (strip boards), grown on demand
   size_t scr_floats = 0;
   std::vector<void*> allocs;
+  // move-parallel launch timing (mzgo_selfplay_set_timing): per launch pair,
+  // events before the boards launch, between it and k_search_queue, after it
+  bool timing = false;
+  std::vector<hipEvent_t> tev;
+  int tn = 0;                   // launch pairs recorded since the last read
   int64_t bytes = 0;
   int epoch = 0;
   const double* noise = nullptr;
@@ -235,6 +255,7 @@ struct mzgo_engine {
       tower->free_batch();
       delete tower;
     }
+    for (hipEvent_t ev : tev) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
     if (d_w) (void)hipFree(d_w);
     if (d_scr) (void)hipFree(d_scr);
@@ -405,14 +426,24 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   EngineArrays& E = e->E;
   E.S = e->S;
   E.max_moves = e->M;
-  const size_t G = e->G, n1 = (size_t)e->S + 1, A = e->A, CELLS = e->CELLS, M = e->M;
+  // Search-tree slots.  Boards whose game-per-workgroup launch takes helper
+  // workgroups (19x19: fewer games than CUs, 3 helpers each) get a tree per
+  // CU when the move-parallel epoch can run (compat "reference", self_play.py
+  // search): its queue runs one search per CU (k_search_queue).
+  // MZGO_MOVE_PARALLEL=0 at creation keeps G.
+  e->TS = e->G;
+  if (C != 0 && !TW && ks->shared_batches && cfg->compat == 0 && cfg->search_variant == 0) {
+    const char* v = getenv("MZGO_MOVE_PARALLEL");
+    if (!(v && atoi(v) == 0)) e->TS = std::max(e->G, device_cus());
+  }
+  const size_t G = e->G, TSL = e->TS, n1 = (size_t)e->S + 1, A = e->A, CELLS = e->CELLS, M = e->M;
   int rc = MZGO_OK;
   auto chk = [&](int r) { if (r != MZGO_OK && rc == MZGO_OK) rc = r; };
   if (C != 0 && !TW) {
     // S+1 node slots + one scratch latent per game
-    chk(e->alloc(&E.pool, G * (n1 + 1) * (size_t)C * e->CS));
+    chk(e->alloc(&E.pool, TSL * (n1 + 1) * (size_t)C * e->CS));
     // pad cells (>= N*N) of pooled latents are read as zeros and never written
-    if (rc == MZGO_OK && hipMemset(E.pool, 0, G * (n1 + 1) * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
+    if (rc == MZGO_OK && hipMemset(E.pool, 0, TSL * (n1 + 1) * (size_t)C * e->CS * sizeof(float)) != hipSuccess)
       chk(fail(MZGO_EHIP, "hipMemset(pool) failed"));
   }
   if (TW) {
@@ -469,15 +500,16 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     }
   }
   if (C != 0) {
-    chk(e->alloc(&E.prior, G * n1 * A));
-    chk(e->alloc(&E.child, G * n1 * A));
-    chk(e->alloc(&E.visits, G * n1));
-    chk(e->alloc(&E.wsum, G * n1));
-    chk(e->alloc(&E.root_prior, G * A));
-    chk(e->alloc(&E.path, G * (n1 + 1)));
-    chk(e->alloc(&E.nodes, G));
-    chk(e->alloc(&E.nact, G * n1));
+    chk(e->alloc(&E.prior, TSL * n1 * A));
+    chk(e->alloc(&E.child, TSL * n1 * A));
+    chk(e->alloc(&E.visits, TSL * n1));
+    chk(e->alloc(&E.wsum, TSL * n1));
+    chk(e->alloc(&E.root_prior, TSL * A));
+    chk(e->alloc(&E.path, TSL * (n1 + 1)));
+    chk(e->alloc(&E.nodes, TSL));
+    chk(e->alloc(&E.nact, TSL * n1));
     chk(e->alloc(&E.jobs, (size_t)G * job_bytes(A)));
+    chk(e->alloc(&E.mpq, 2 * (size_t)G + 1));
     chk(e->alloc(&E.rec_stones, G * M * CELLS));
     chk(e->alloc(&E.rec_invd, G * M * CELLS));
     chk(e->alloc(&E.rec_flags, G * M));
@@ -495,8 +527,8 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
   chk(e->alloc(&E.counters, kCounters));
   chk(e->alloc(&e->d_err, 1));
 #ifdef MZGO_STAMPS
-  chk(e->alloc(&E.stamps, G * kStampPhases));
-  if (E.stamps) (void)hipMemset(E.stamps, 0, G * kStampPhases * 8);
+  chk(e->alloc(&E.stamps, TSL * kStampPhases));
+  if (E.stamps) (void)hipMemset(E.stamps, 0, TSL * kStampPhases * 8);
 #endif
   if (rc != MZGO_OK) { delete e; return rc; }
   if (hipMemset(E.counters, 0, kCounters * sizeof(unsigned long long)) != hipSuccess ||
@@ -709,18 +741,6 @@ int mzgo_selfplay_reset(mzgo_engine* e, int epoch, void* stream) {
 // k_selfplay_move; boards whose batch expansions stream Y from L2 (19x19) get
 // helper workgroups, 3 per game by default (MZGO_HELPERS_PER_GAME), with the
 // job slots zeroed before the launch (batch_expand_shared)
-// CUs of the current device (one self-play workgroup fills a CU's LDS)
-static int device_cus() {
-  static int ncu[64];                  // per device ordinal (0: not read yet)
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (ncu[dev] <= 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
-    ncu[dev] = n;
-  }
-  return ncu[dev];
-}
 
 // The epoch tail (whole-game launches): a workgroup whose game has ended
 // stays resident and serves running games.  Only when every workgroup of the
@@ -739,8 +759,43 @@ static bool tail_enabled(int workgroups) {
   return mode == 2 || workgroups <= device_cus();
 }
 
-static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayParams& pp, hipStream_t s) {
+// The move-parallel epoch (k_search_queue): multi-move launches under compat
+// "reference" play the boards first and then run every recorded move's search
+// from one queue, one workgroup per CU (no helper workgroups: at 19x19 every
+// CU runs its own search instead of a game's 4 workgroups sharing one); the
+// records are the same as the game-per-workgroup launch's.
+// MZGO_MOVE_PARALLEL=0 keeps the game-per-workgroup launch (its epoch tail:
+// tail_help / join_running_game).
+static bool move_parallel(const mzgo_engine* e, const SearchParams& sp, const PlayParams& pp) {
+  const char* v = getenv("MZGO_MOVE_PARALLEL");
+  if (v && atoi(v) == 0) return false;
+  return pp.moves > 1 && !pp.arena && sp.compat == 0 && sp.variant == 0;
+}
+
+static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayParams& pp_in, hipStream_t s) {
   SearchParams sp = e->search_params();
+  PlayParams pp = pp_in;
+  if (move_parallel(e, sp, pp)) {
+    pp.boards_only = 1;
+    hipEvent_t* ev = nullptr;
+    if (e->timing) {
+      while ((int)e->tev.size() < 3 * (e->tn + 1)) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreate(&x));
+        e->tev.push_back(x);
+      }
+      ev = &e->tev[3 * e->tn++];
+    }
+    HIPCHK(hipMemsetAsync(e->E.mpq + 2 * e->G, 0, sizeof(int), s));
+    if (ev) HIPCHK(hipEventRecord(ev[0], s));
+    HIPCHK(e->ks->selfplay_move(e->np, np_b, sp, pp, e->E, e->G, s));
+    if (ev) HIPCHK(hipEventRecord(ev[1], s));
+    const int ncu = device_cus();
+    const int wg = ncu > 0 && ncu < e->TS ? ncu : e->TS;     // one tree slot per workgroup
+    HIPCHK(e->ks->search_queue(e->np, sp, pp, e->E, e->G, wg, s));
+    if (ev) HIPCHK(hipEventRecord(ev[2], s));
+    return MZGO_OK;
+  }
   if (e->ks->shared_batches) {
     int per = 3;
     if (const char* v = getenv("MZGO_HELPERS_PER_GAME")) per = atoi(v);
@@ -759,6 +814,26 @@ static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayPara
 }
 
 int mzgo_selfplay_move(mzgo_engine* e, void* stream) { return mzgo_selfplay_moves(e, 1, stream); }
+
+int mzgo_selfplay_set_timing(mzgo_engine* e, int on) {
+  if (!e) return fail(MZGO_EINVAL, "bad argument");
+  e->timing = on != 0;
+  e->tn = 0;
+  return MZGO_OK;
+}
+
+int mzgo_selfplay_launch_times(mzgo_engine* e, float* boards_ms, float* queue_ms, int cap, int* n_host) {
+  if (!e || !n_host || cap < 0 || (cap > 0 && (!boards_ms || !queue_ms))) return fail(MZGO_EINVAL, "bad argument");
+  const int n = e->tn < cap ? e->tn : cap;
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipEventSynchronize(e->tev[3 * i + 2]));
+    HIPCHK(hipEventElapsedTime(&boards_ms[i], e->tev[3 * i], e->tev[3 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&queue_ms[i], e->tev[3 * i + 1], e->tev[3 * i + 2]));
+  }
+  *n_host = e->tn;
+  e->tn = 0;
+  return MZGO_OK;
+}
 
 int mzgo_selfplay_moves(mzgo_engine* e, int moves, void* stream) {
   if (!e || e->C == 0 || moves < 1) return fail(MZGO_EINVAL, "bad argument");

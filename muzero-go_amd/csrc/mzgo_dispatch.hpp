@@ -25,6 +25,8 @@ struct KernelSet {
   hipError_t (*board_planes)(const EngineArrays&, int G, double* planes, hipStream_t);
   hipError_t (*selfplay_move)(const NetParams& np, const NetParams& np_b, const SearchParams&,
                               const PlayParams&, const EngineArrays&, int G, hipStream_t);
+  hipError_t (*search_queue)(const NetParams& np, const SearchParams&, const PlayParams&, const EngineArrays&,
+                             int G, int workgroups, hipStream_t);
 };
 
 const KernelSet* find_kernels(int N, int C);
@@ -69,12 +71,17 @@ struct Launch {
                        pp, E);
     return hipGetLastError();
   }
+  static hipError_t queue(const NetParams& np, const SearchParams& sp, const PlayParams& pp, const EngineArrays& E,
+                          int G, int workgroups, hipStream_t s) {
+    hipLaunchKernelGGL((k_search_queue<N, C>), dim3(workgroups), dim3(Geo<N, C>::THREADS), 0, s, np, sp, pp, E, G);
+    return hipGetLastError();
+  }
   static KernelSet table() {
     typedef Geo<N, C> G;
     return KernelSet{N, C, sizeof(Smem<G>), rep_needs_scratch<G>() ? 64 * N * N : 0,
                      Smem<G>::GLOBAL_Y ? 1 : 0, TailConvs<G>::value ? 1 : 0, &ii, &ri, &search, &breset, &bstep,
                      &bplanes,
-                     &move};
+                     &move, &queue};
   }
 };
 

@@ -111,6 +111,8 @@ struct EngineArrays {
   double* final_reward;  // [G]
   int* status;           // [G]  0 playing, 1 finished, >=16 error
   unsigned char* jobs;   // [G][job_bytes(A)] batch-expansion jobs shared with helper workgroups
+  int* mpq;              // [2G + 1] move-parallel epoch (k_search_queue): per game (first move,
+                         // moves played) of the boards-only launch, then the queue head
   unsigned long long* counters;  // [kCounters] 0: simulations run, 1: moves played, 2: games finished,
                                  //     3: dynamics convs run (factored: one per new parent; tower
                                  //     engines: towers evaluated, speculative ones included),
@@ -127,7 +129,7 @@ __device__ __forceinline__ EngineArrays launder_arrays(const EngineArrays& e) {
   MZGO_L(pool) MZGO_L(prior) MZGO_L(child) MZGO_L(visits) MZGO_L(wsum) MZGO_L(root_prior) MZGO_L(path)
   MZGO_L(nodes) MZGO_L(nact) MZGO_L(stones) MZGO_L(invd) MZGO_L(meta) MZGO_L(rec_stones) MZGO_L(rec_invd)
   MZGO_L(rec_flags) MZGO_L(rec_action) MZGO_L(rec_value) MZGO_L(rec_policy) MZGO_L(rec_reward) MZGO_L(game_len)
-  MZGO_L(final_reward) MZGO_L(status) MZGO_L(jobs) MZGO_L(counters) MZGO_L(stamps)
+  MZGO_L(final_reward) MZGO_L(status) MZGO_L(jobs) MZGO_L(mpq) MZGO_L(counters) MZGO_L(stamps)
 #undef MZGO_L
   return r;
 }
@@ -2451,6 +2453,9 @@ struct PlayParams {
   int arena;              // 0: one network; 1: main.py's evaluator -- game i's first
                           // mover is network (i % 2), then the networks alternate
   int moves;              // moves per game in this launch (each game stops at its end)
+  int boards_only = 0;    // 1: the move-parallel epoch's first launch -- record, choose (compat
+                          // "reference": the action never reads the search) and step every
+                          // move, no search; k_search_queue then runs the searches
 };
 
 template <int N, int C>
@@ -2510,12 +2515,15 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #endif
       }
   };
+  if (pp.boards_only && tid_local() == 0) E_arg.mpq[2 * g + 1] = 0;
   if (E.status[g] != 0) { release_helpers(); tail_phase(); return; }
   if ((sp.helpers > 0 || sp.tail) && tid_local() == 0)
     __hip_atomic_store(job_of<G>(E_arg, g).started(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   BoardMeta m;
   load_board<G>(sm, E, g, m);
+  const int mv_first = m.moves;
+  int played = 0;                                // moves recorded by this launch
   // pp.moves moves of this game in one launch (the board stays in LDS between
   // them): a game's moves run back to back on its CU instead of every move of
   // every game waiting for the slowest game's move at a launch boundary
@@ -2542,6 +2550,7 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     E.rec_invd[rec * G::CELLS + c] = sm.invd[c];
   }
   if (tid_local() == 0) E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
+  ++played;
 
   const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
   const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
@@ -2553,8 +2562,11 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #endif
   SearchParams spm = launder_search(sp);
   spm.net = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? 1 : 0;
-  run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
-                tm ? tm + 2 : nullptr, noise_out);
+  if (pp.boards_only)
+    build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return board_plane<G>(sm, m0, 3, a); });
+  else
+    run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
+                  tm ? tm + 2 : nullptr, noise_out);
 #ifdef MZGO_STAMPS
   tm[4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -2567,8 +2579,10 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     if (lane_id_local() == 0) {
       sm.bc[0] = a;
       E.rec_action[rec] = a;
-      const int n = T.visits[0];
-      E.rec_value[rec] = n > 0 ? T.wsum[0] / (double)n : 0.0;
+      if (!pp.boards_only) {                       // (the move-parallel epoch: k_search_queue)
+        const int n = T.visits[0];
+        E.rec_value[rec] = n > 0 ? T.wsum[0] / (double)n : 0.0;
+      }
     }
   }
   __syncthreads();
@@ -2612,8 +2626,74 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if (over) break;
   __syncthreads();                               // this move's LDS reads before the next move's writes
   }
+  // the moves this launch recorded (an erroring move included: it was searched)
+  if (pp.boards_only && tid_local() == 0) {
+    E_arg.mpq[2 * g] = mv_first;
+    E_arg.mpq[2 * g + 1] = played;
+  }
   release_helpers();
   tail_phase();
+}
+
+// ---------------------------------------------------------------------------
+// The move-parallel epoch, second launch (compat "reference", SURVEY.md §0.6:
+// the action is a uniform draw over the legal moves and the policy target is
+// mask / sum, so a game's board sequence never reads its searches and every
+// (game, move) search is independent once the boards are played).  A
+// persistent grid of one workgroup per CU claims (game, move) items from one
+// queue -- the moves of every game, latest first -- and runs each search in
+// its own tree slot (blockIdx.x) from the recorded observation; the search's
+// root value is the record's.  The same searches, keys and noise as the
+// game-per-workgroup launch, so the records are identical; the epoch's tail
+// (a game's whole remaining move sequence on one CU while the others idle)
+// shrinks to one search.
+// ---------------------------------------------------------------------------
+template <int N, int C>
+__global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_waves_per_eu(Geo<N, C>::WPE, Geo<N, C>::WPE))) k_search_queue(NetParams np_arg, SearchParams sp, PlayParams pp,
+                                                            EngineArrays E_arg, int games) {
+  typedef Geo<N, C> G;
+  __shared__ Smem<G> sm;
+  static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
+  if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
+  const int slot = blockIdx.x;
+  const int items = games * pp.moves;
+  for (;;) {
+    if (tid_local() == 0) sm.bc[0] = (int)atomicAdd((unsigned*)&E_arg.mpq[2 * games], 1u);
+    __syncthreads();
+    const int k = sm.bc[0];
+    __syncthreads();                               // (sm.bc is the search's scratch too)
+    if (k >= items) break;
+    const int j = k / games, g = k % games;
+    const int mv0 = __builtin_amdgcn_readfirstlane(E_arg.mpq[2 * g]);
+    const int nmv = __builtin_amdgcn_readfirstlane(E_arg.mpq[2 * g + 1]);
+    if (j >= nmv) continue;
+    const int mv = mv0 + nmv - 1 - j;
+    const EngineArrays E = launder_arrays(E_arg);
+    const NetParams np = launder_params(np_arg);
+    const size_t rec = (size_t)g * E.max_moves + mv;
+    for (int c = tid_local(); c < G::CELLS; c += G::THREADS) {
+      sm.stone[c] = E.rec_stones[rec * G::CELLS + c];
+      sm.invd[c] = E.rec_invd[rec * G::CELLS + c];
+    }
+    const int fl = E.rec_flags[rec];
+    BoardMeta m0;
+    m0.turn = fl & 1; m0.passed = (fl >> 1) & 1; m0.done = (fl >> 2) & 1; m0.moves = mv;
+    __syncthreads();
+    const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
+    const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
+    const double* noise = pp.noise ? pp.noise + rec * G::A : nullptr;
+    double* noise_out = pp.noise_out ? pp.noise_out + rec * G::A : nullptr;
+    SearchParams spm = launder_search(sp);
+    spm.net = 0;
+    run_search<G>(sm, np, spm, E, slot, [&](int c, int jj) { return board_plane<G>(sm, m0, c, jj); }, noise, key,
+                  nullptr, noise_out);
+    if (tid_local() == 0) {
+      const TreeView T = TreeViewOf<G>::make(E, slot);
+      const int n = T.visits[0];
+      E.rec_value[rec] = n > 0 ? T.wsum[0] / (double)n : 0.0;
+    }
+    __syncthreads();                               // this search's LDS reads before the next board
+  }
 }
 
 }  // namespace mzgo

@@ -71,6 +71,8 @@ SIGNATURES = {
     "mzgo_arena_move": (_I, [_P, _P, _P]),
     "mzgo_arena_moves": (_I, [_P, _P, _I, _P]),
     "mzgo_selfplay_counters": (_I, [_P, _P, _P]),
+    "mzgo_selfplay_set_timing": (_I, [_P, _I]),
+    "mzgo_selfplay_launch_times": (_I, [_P, _P, _P, _I, _P]),
     "mzgo_stream_wait_started": (_I, [_P, ctypes.c_uint64, _P]),
     "mzgo_tower_timing": (_I, [_P, _I, _P, _P]),
     "mzgo_selfplay_inject_noise": (_I, [_P, _P]),

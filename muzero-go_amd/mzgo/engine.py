@@ -240,6 +240,19 @@ class Engine:
         check(lib.mzgo_tower_timing(self._h, int(enable), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def launch_timing(self, enable):
+        """Move-parallel epochs (mzgo_selfplay_launch_times): the (boards, queue)
+        launch durations in ms of every multi-move call since the last read
+        (synchronises; empty lists when none ran), then timing on/off."""
+        cap = 4096
+        b = np.zeros(cap, np.float32)
+        q = np.zeros(cap, np.float32)
+        n = ctypes.c_int()
+        check(lib.mzgo_selfplay_launch_times(self._h, ptr(b), ptr(q), cap, ctypes.byref(n)))
+        check(lib.mzgo_selfplay_set_timing(self._h, int(enable)))
+        k = min(n.value, cap)
+        return b[:k].tolist(), q[:k].tolist()
+
     def counters(self):
         out = np.zeros(9, np.uint64)
         check(lib.mzgo_selfplay_counters(self._h, ptr(out), stream_of(self.device)))

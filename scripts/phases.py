@@ -52,6 +52,10 @@ def _decile(f, game, sp):
 
 
 def main():
+    # the game-per-workgroup launch (one game's whole epoch per workgroup: the
+    # tail this script measures); the move-parallel epoch's queue has no
+    # per-game workgroups
+    os.environ.setdefault("MZGO_MOVE_PARALLEL", "0")
     import mzgo
     from mzgo import _lib
     tag = sys.argv[1] if len(sys.argv) > 1 else "phases"

@@ -285,6 +285,7 @@ def test_tail_helpers_do_not_change_records(epoch, monkeypatch):
     sp = __import__("mzgo").SelfPlay(net, G, S, seed=SEED)
     eng = sp.engine
     out = {}
+    monkeypatch.setenv("MZGO_MOVE_PARALLEL", "0")     # (the game-per-workgroup launch has the tail)
     for on in ("1", "0"):
         monkeypatch.setenv("MZGO_TAIL_HELPERS", on)
         c0 = eng.counters()
@@ -315,6 +316,7 @@ def test_tail_helpers_games_above_cu_count(monkeypatch):
     sp = mzgo.SelfPlay(net, G, S, seed=SEED)
     eng = sp.engine
     out = {}
+    monkeypatch.setenv("MZGO_MOVE_PARALLEL", "0")
     for mode in ("1", "2", "0"):
         monkeypatch.setenv("MZGO_TAIL_HELPERS", mode)
         c0 = eng.counters()
@@ -331,3 +333,59 @@ def test_tail_helpers_games_above_cu_count(monkeypatch):
             {k: v for k, v in out["0"][1].items() if k not in ("tail_convs", "tail_wait_expiries")}
         for k in a:
             np.testing.assert_array_equal(a[k].view(np.uint8), out["0"][0][k].view(np.uint8), err_msg=f"{mode} {k}")
+
+
+MP_CASES = [
+    # N, G, S, moves per launch (0: the whole game), epoch
+    (9, 256, 200, 0, 4),       # the headline's own launch
+    (9, None, 8, 16, 2),       # more games than CUs (the queue's grid is the CU count), chunked launches
+    (5, 64, 50, 0, 1),
+    (19, 16, 96, 0, 1),        # 19x19: a tree slot per CU (k_search_queue) vs 3 helper workgroups per game
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("N,G,S,per,epoch", MP_CASES, ids=["9x9_g256_s200", "9x9_gcu44_s8_chunk16", "5x5_g64_s50", "19x19_g16_s96"])
+def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, monkeypatch):
+    """The move-parallel epoch (compat "reference"; k_selfplay_move boards-only,
+    then k_search_queue: every recorded move's search claimed from one queue by
+    a grid of one workgroup per CU, each in its own tree slot) against the
+    game-per-workgroup launch (MZGO_MOVE_PARALLEL=0): byte-identical records
+    (observations, actions, root values, policies, rewards, lengths, status),
+    the same Dirichlet sample at every root (test hook) and the same counters
+    -- the same searches under the same keys, only scheduled differently."""
+    import mzgo
+    if G is None:
+        G = torch.cuda.get_device_properties(0).multi_processor_count + 44
+    net = _net(N)
+    sp = mzgo.SelfPlay(net, G, S, seed=SEED)
+    eng = sp.engine
+    M = sp.max_moves
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MZGO_MOVE_PARALLEL", mode)
+        monkeypatch.setenv("MZGO_TAIL_HELPERS", "0")
+        drawn = torch.zeros(G, M, eng.A, dtype=torch.float64, device="cuda")
+        eng.record_noise(drawn)
+        c0 = eng.counters()
+        sp.reset(epoch=epoch)
+        step = per or M
+        for j in range(0, M, step):
+            sp.move(min(step, M - j))
+        c1 = eng.counters()
+        eng.record_noise(None)
+        recs, arrays = _records(eng)
+        out[mode] = (arrays, drawn.cpu().numpy(),
+                     {k: c1[k] - c0[k] for k in c1 if k not in ("playing", "tail_wait_expiries")})
+    (aa, da, ca), (ab, db, cb) = out["1"], out["0"]
+    if N == 19:
+        # prior_rows counts the rows a game's own workgroup forms; with helper
+        # workgroups (the game-per-workgroup launch at 19x19) the batch
+        # expansions' rows are formed by job and not counted there
+        ca.pop("prior_rows"), cb.pop("prior_rows")
+    assert ca == cb, (ca, cb)
+    assert ca["games_finished"] == G and ca["simulations"] == ca["moves"] * S
+    for k in aa:
+        np.testing.assert_array_equal(aa[k].view(np.uint8), ab[k].view(np.uint8), err_msg=k)
+    np.testing.assert_array_equal(da.view(np.uint64), db.view(np.uint64))
+    assert (aa["meta"][:, 3] > 0).all()
