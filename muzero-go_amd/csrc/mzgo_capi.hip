@@ -508,7 +508,7 @@ int mzgo_engine_create(const mzgo_config* cfg, mzgo_engine** out) {
     chk(e->alloc(&E.path, TSL * (n1 + 1)));
     chk(e->alloc(&E.nodes, TSL));
     chk(e->alloc(&E.nact, TSL * n1));
-    chk(e->alloc(&E.jobs, (size_t)G * job_bytes(A)));
+    chk(e->alloc(&E.jobs, TSL * job_bytes(A)));
     chk(e->alloc(&E.mpq, 2 * (size_t)G + 1));
     chk(e->alloc(&E.rec_stones, G * M * CELLS));
     chk(e->alloc(&E.rec_invd, G * M * CELLS));
@@ -791,7 +791,19 @@ static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayPara
     HIPCHK(e->ks->selfplay_move(e->np, np_b, sp, pp, e->E, e->G, s));
     if (ev) HIPCHK(hipEventRecord(ev[1], s));
     const int ncu = device_cus();
-    const int wg = ncu > 0 && ncu < e->TS ? ncu : e->TS;     // one tree slot per workgroup
+    int wg = ncu > 0 && ncu < e->TS ? ncu : e->TS;           // one tree slot per workgroup
+    // 19x19: MZGO_QUEUE_HELPERS=h gives every searching workgroup h helpers
+    // (wg / (1 + h) searches at once, each tree slot's jobs shared)
+    if (e->ks->shared_batches) {
+      const char* v = getenv("MZGO_QUEUE_HELPERS");
+      const int h = v ? atoi(v) : 0;
+      if (h > 0 && wg / (1 + h) >= 1) {
+        const int leaders = wg / (1 + h);
+        sp.helpers = h * leaders;
+        wg = leaders * (1 + h);
+        HIPCHK(hipMemsetAsync(e->E.jobs, 0, (size_t)leaders * job_bytes(e->A), s));
+      }
+    }
     HIPCHK(e->ks->search_queue(e->np, sp, pp, e->E, e->G, wg, s));
     if (ev) HIPCHK(hipEventRecord(ev[2], s));
     return MZGO_OK;

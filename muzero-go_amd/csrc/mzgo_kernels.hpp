@@ -2655,6 +2655,16 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   __shared__ Smem<G> sm;
   static_assert(sizeof(Smem<G>) <= 160 * 1024, "one workgroup per CU: the whole LDS at most");
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
+  // sp.helpers > 0 (19x19, MZGO_QUEUE_HELPERS): the first gridDim.x /
+  // (1 + helpers per leader) workgroups claim searches, the others serve a
+  // leader's batch expansions and parent convs as jobs (helper_loop) for the
+  // whole launch, as a game's helpers do in the game-per-workgroup launch
+  const int leaders = (int)gridDim.x - sp.helpers;
+  if ((int)blockIdx.x >= leaders) {
+    if constexpr (Smem<G>::GLOBAL_Y && G::WINO)
+      helper_loop<G>(sm, np_arg, np_arg, sp, E_arg, ((int)blockIdx.x - leaders) % leaders);
+    return;
+  }
   const int slot = blockIdx.x;
   const int items = games * pp.moves;
   for (;;) {
@@ -2694,6 +2704,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     }
     __syncthreads();                               // this search's LDS reads before the next board
   }
+  if (sp.helpers > 0 && tid_local() == 0)
+    __hip_atomic_store(job_of<G>(E_arg, slot).seq(), kJobExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace mzgo

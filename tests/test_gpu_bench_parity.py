@@ -336,17 +336,19 @@ def test_tail_helpers_games_above_cu_count(monkeypatch):
 
 
 MP_CASES = [
-    # N, G, S, moves per launch (0: the whole game), epoch
-    (9, 256, 200, 0, 4),       # the headline's own launch
-    (9, None, 8, 16, 2),       # more games than CUs (the queue's grid is the CU count), chunked launches
-    (5, 64, 50, 0, 1),
-    (19, 16, 96, 0, 1),        # 19x19: a tree slot per CU (k_search_queue) vs 3 helper workgroups per game
+    # N, G, S, moves per launch (0: the whole game), epoch, MZGO_QUEUE_HELPERS
+    (9, 256, 200, 0, 4, "0"),       # the headline's own launch
+    (9, None, 8, 16, 2, "0"),       # more games than CUs (the queue's grid is the CU count), chunked launches
+    (5, 64, 50, 0, 1, "0"),
+    (19, 16, 96, 0, 1, "0"),        # 19x19: a tree slot per CU (k_search_queue) vs 3 helper workgroups per game
+    (19, 16, 96, 0, 2, "1"),        # 19x19: every searching workgroup with a helper (jobs per tree slot)
 ]
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("N,G,S,per,epoch", MP_CASES, ids=["9x9_g256_s200", "9x9_gcu44_s8_chunk16", "5x5_g64_s50", "19x19_g16_s96"])
-def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, monkeypatch):
+@pytest.mark.parametrize("N,G,S,per,epoch,qh", MP_CASES, ids=["9x9_g256_s200", "9x9_gcu44_s8_chunk16", "5x5_g64_s50",
+                                                            "19x19_g16_s96", "19x19_g16_s96_qh1"])
+def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, qh, monkeypatch):
     """The move-parallel epoch (compat "reference"; k_selfplay_move boards-only,
     then k_search_queue: every recorded move's search claimed from one queue by
     a grid of one workgroup per CU, each in its own tree slot) against the
@@ -362,6 +364,7 @@ def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, monk
     eng = sp.engine
     M = sp.max_moves
     out = {}
+    monkeypatch.setenv("MZGO_QUEUE_HELPERS", qh)
     for mode in ("1", "0"):
         monkeypatch.setenv("MZGO_MOVE_PARALLEL", mode)
         monkeypatch.setenv("MZGO_TAIL_HELPERS", "0")
