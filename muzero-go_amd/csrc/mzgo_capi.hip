@@ -1055,7 +1055,7 @@ int mzgo_records_export(mzgo_engine* e, int g, int32_t* length, int32_t* status,
 // Diagnostic build only: copy (and zero) the per-slot phase cycle sums.
 int mzgo_debug_stamps(mzgo_engine* e, unsigned long long* host) {
   if (!e || !e->E.stamps) return fail(MZGO_EINVAL, "no stamps");
-  const size_t n = (size_t)e->G * kStampPhases;
+  const size_t n = (size_t)e->TS * kStampPhases;     // every tree slot's row (TS >= G)
   HIPCHK(hipMemcpy(host, e->E.stamps, n * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemset(e->E.stamps, 0, n * 8));
   return MZGO_OK;

@@ -55,7 +55,7 @@ struct ExpandLds {
   static constexpr int BASE = YC + 3 * G::CS + 3 * G::C;
   static constexpr bool CACHE = BASE <= UF;
   static constexpr int PERW = 3 * G::CS + 9 * G::C + 3 * 64 * G::AP;   // one wave's batch buffers
-  static constexpr int PERW_G = G::CS + 9 * G::C;                      // ... with Y streamed from L2
+  static constexpr int PERW_G = G::CS + 18 * G::C;                     // ... with Y streamed from L2 (two E rows)
   static_assert(CACHE || 9 * G::C >= 2 * 64 * G::AP, "E's space holds child_priors' scratch (f32 then f64, in turn)");
   // tail arrays: bv (A+16 doubles = 2(A+16) floats) and acts (A ints)
   static constexpr int TAIL = 2 * (G::A + 16) + G::A + 64;
@@ -74,6 +74,7 @@ struct ExpandLds {
   struct Wave {
     alignas(16) float xw[XW];             // the child's policy sums per cell (at PROW)
     alignas(16) float ew[9 * G::C];       // E[a] of the child
+    alignas(16) float ew2[CACHE ? 4 : 9 * G::C];   // (Y streamed from L2) E[a] of the pair's second child
     float fb[CACHE ? 64 * G::AP : 1];     // ordered-sum scratch (child_priors)
     double db[CACHE ? 64 * G::AP : 1];
     __device__ float* fscratch() { if constexpr (CACHE) return fb; else return ew; }
@@ -335,6 +336,121 @@ __device__ __forceinline__ void expand_wave(float* xw, const float* yc, const fl
   }
   rsum = wave_sum(dr2.x + dr2.y);
   vsum = wave_sum(dv2.x + dv2.y);
+}
+
+// Two children of one parent by ONE wave, Y streamed from L2 (GLOBAL_Y
+// boards, 19x19; expand_wave's pass-pair loop): every Y value a lane loads
+// serves both children, so a batch reads its parent's Y (139 KB at 19x19)
+// once per pair of children instead of once per child.  Per child the
+// operations and their order are expand_wave<..., true>'s, so both results
+// are bit-identical to two expand_wave calls: child 0's policy sums go to
+// xw[PROW + cell] as there; child 1's stay in registers, lane j of a lane
+// group keeping passes p = j (mod 8) (pol1[p / 8]; its 8 lanes hold the same
+// sum), until store_policy2 writes them over child 0's row.
+template <class G>
+struct Pol2 {
+  static constexpr int SLOTS = (ExpandPlan<G>::PASSES + 7) / 8;
+  float v[SLOTS];
+};
+template <class G, int PROW>
+__device__ __forceinline__ void expand_wave2(float* xw, const float* yc, const float* ew0, const float* ew1,
+                                             const float* hw, const ExpandPlan<G>& plan, float& rsum0,
+                                             float& vsum0, float& rsum1, float& vsum1, Pol2<G>& pol1) {
+  typedef ExpandShape<G> X;
+  constexpr int P = ExpandPlan<G>::PASSES;
+  static_assert(!ExpandPlan<G>::TABLE && P % 2 == 0, "the pass-pair loop of Y-streaming boards");
+  const int lane = lane_id_local();
+  const int j = lane & 7, cg = lane >> 3;
+  const f32x4* W4 = reinterpret_cast<const f32x4*>(hw);
+  f32x4 wp[X::PERL];
+  f32x2 sa[X::PERL][2], sb[X::PERL][2];
+#pragma unroll
+  for (int k = 0; k < X::PERL; ++k) {
+    wp[k] = W4[2 * X::C4 + j + 8 * k];
+    sa[k][0] = sa[k][1] = sb[k][0] = sb[k][1] = f32x2{0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < Pol2<G>::SLOTS; ++i) pol1.v[i] = 0.f;
+  const f32x4* Y4 = reinterpret_cast<const f32x4*>(yc) + cg * X::C4 + j;
+  const char* Eb0 = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew0) + j);
+  const char* Eb1 = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew1) + j);
+  float* xr = xw + PROW + cg;
+  auto pass_y = [&](int p, const f32x4 (&y)[X::PERL], uint32_t eoff, bool last) {
+    const f32x4* E0 = reinterpret_cast<const f32x4*>(Eb0 + eoff);
+    const f32x4* E1 = reinterpret_cast<const f32x4*>(Eb1 + eoff);
+    f32x4 e0[X::PERL], e1[X::PERL];
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) { e0[k] = E0[8 * k]; e1[k] = E1[8 * k]; }
+    const bool live = G::CELLS % 8 == 0 || !last || cg + 8 * p < G::CELLS;
+    f32x2 ha = {0.f, 0.f}, hb = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) {
+#pragma unroll
+      for (int q = 0; q < 4; q += 2) {
+        const f32x2 yy = f32x2{y[k][q], y[k][q + 1]};
+        const f32x2 w2 = f32x2{wp[k][q], wp[k][q + 1]};
+        f32x2 va = yy + f32x2{e0[k][q], e0[k][q + 1]};
+        va.x = va.x > 0.f ? va.x : 0.f;
+        va.y = va.y > 0.f ? va.y : 0.f;
+        ha = __builtin_elementwise_fma(w2, va, ha);
+        if (!live) va = f32x2{0.f, 0.f};
+        sa[k][q >> 1] = sa[k][q >> 1] + va;
+        f32x2 vb = yy + f32x2{e1[k][q], e1[k][q + 1]};
+        vb.x = vb.x > 0.f ? vb.x : 0.f;
+        vb.y = vb.y > 0.f ? vb.y : 0.f;
+        hb = __builtin_elementwise_fma(w2, vb, hb);
+        if (!live) vb = f32x2{0.f, 0.f};
+        sb[k][q >> 1] = sb[k][q >> 1] + vb;
+      }
+    }
+    xr[8 * p] = sum8(ha.x + ha.y);
+    const float pb = sum8(hb.x + hb.y);
+#pragma unroll
+    for (int i = 0; i < Pol2<G>::SLOTS; ++i) pol1.v[i] = p == 8 * i + j ? pb : pol1.v[i];
+  };
+  f32x4 ya[X::PERL], yb[X::PERL];
+  auto ldy = [&](int p, f32x4 (&y)[X::PERL]) {
+#pragma unroll
+    for (int k = 0; k < X::PERL; ++k) y[k] = Y4[p * 8 * X::C4 + 8 * k];
+  };
+  ldy(0, ya);
+#pragma unroll 1
+  for (int pp = 0; pp < P / 2; ++pp) {
+    const uint32_t w2 = plan.pair(pp, cg);
+    ldy(2 * pp + 1, yb);
+    pass_y(2 * pp, ya, w2 & 0xFFFFu, false);
+    if (pp + 1 < P / 2) ldy(2 * pp + 2, ya);
+    pass_y(2 * pp + 1, yb, w2 >> 16, pp + 1 == P / 2);
+  }
+  f32x2 ra = {0.f, 0.f}, va2 = {0.f, 0.f}, rb = {0.f, 0.f}, vb2 = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < X::PERL; ++k) {
+    const f32x4 wr = W4[j + 8 * k], wv = W4[X::C4 + j + 8 * k];
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      ra = __builtin_elementwise_fma(f32x2{wr[q], wr[q + 1]}, sa[k][q >> 1], ra);
+      va2 = __builtin_elementwise_fma(f32x2{wv[q], wv[q + 1]}, sa[k][q >> 1], va2);
+      rb = __builtin_elementwise_fma(f32x2{wr[q], wr[q + 1]}, sb[k][q >> 1], rb);
+      vb2 = __builtin_elementwise_fma(f32x2{wv[q], wv[q + 1]}, sb[k][q >> 1], vb2);
+    }
+  }
+  rsum0 = wave_sum(ra.x + ra.y);
+  vsum0 = wave_sum(va2.x + va2.y);
+  rsum1 = wave_sum(rb.x + rb.y);
+  vsum1 = wave_sum(vb2.x + vb2.y);
+}
+
+// child 1's policy sums (expand_wave2's registers) -> xw[PROW + cell]; the
+// caller orders xw (wave_lds_sync) before and after
+template <class G, int PROW>
+__device__ __forceinline__ void store_policy2(float* xw, const Pol2<G>& pol1) {
+  const int lane = lane_id_local();
+  const int j = lane & 7, cg = lane >> 3;
+#pragma unroll
+  for (int i = 0; i < Pol2<G>::SLOTS; ++i) {
+    const int p = 8 * i + j;
+    if (p < ExpandPlan<G>::PASSES) xw[PROW + cg + 8 * p] = pol1.v[i];
+  }
 }
 
 // Lazy policy head.  A batched child's policy logits are read only when a

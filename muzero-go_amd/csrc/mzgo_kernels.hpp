@@ -416,7 +416,68 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
                                              Stamp* st = nullptr) {
   auto& L = sm.u.f;
   typedef decltype(sm.u.f) XL;
-  if constexpr (XL::BATCH) {
+  if constexpr (XL::GLOBAL_Y && !LAZY) {
+    // Y streamed from L2 (19x19): a wave claims two children at a time and
+    // reads the parent's Y once for both (expand_wave2)
+    const int wave = __builtin_amdgcn_readfirstlane(wave_id());
+    const int lane = lane_id_local();
+    auto& W = L.wv[wave];
+    ExpandPlan<G> plan;
+    plan.init(L.rpair);
+    constexpr int E4N = 9 * G::C / 4;
+    f32x4* ew0 = reinterpret_cast<f32x4*>(W.ew);
+    f32x4* ew1 = reinterpret_cast<f32x4*>(W.ew2);
+    // the child's heads, prior row and child row from its totals and the
+    // policy sums in W.xw (as the one-child loop below)
+    auto child_rows = [&](int k, float rsum, float vsum) {
+      const int nid = nid0 + k;
+      float r, v;
+      heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
+      float x[G::AP];
+      policy_logits<G>(W.xw + XL::PROW, sm.t.hsc, x);
+      int* crow = TV.child + (size_t)nid * G::A;
+      for (int i = lane; i < G::A; i += 64) crow[i] = -1;
+      child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
+      if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
+    };
+    for (;;) {
+      int k = 0;
+      if (lane == 0) k = atomicAdd(&sm.t.ngrab, 2);
+      k = __builtin_amdgcn_readfirstlane(k);
+      if (k >= B) break;
+      const bool two = k + 1 < B;
+      const int need = two ? k + 1 : k;
+      while (__hip_atomic_load(&sm.t.npick, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= need)
+        __builtin_amdgcn_s_sleep(2);
+      const int a0 = __builtin_amdgcn_readfirstlane(L.acts[k]);
+      const f32x4* e0 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a0 * 9 * G::C);
+      for (int i = lane; i < E4N; i += 64) ew0[i] = e0[i];
+      if (two) {
+        const int a1 = __builtin_amdgcn_readfirstlane(L.acts[k + 1]);
+        const f32x4* e1 = reinterpret_cast<const f32x4*>(np.etab + (size_t)a1 * 9 * G::C);
+        for (int i = lane; i < E4N; i += 64) ew1[i] = e1[i];
+      }
+      wave_lds_sync();
+      if (two) {
+        float r0, v0, r1, v1;
+        Pol2<G> pol;
+        expand_wave2<G, XL::PROW>(W.xw, yg, W.ew, W.ew2, L.hw, plan, r0, v0, r1, v1, pol);
+        wave_lds_sync();
+        child_rows(k, r0, v0);
+        wave_lds_sync();                     // child k's reads of W.xw / W.ew before child k + 1's
+        store_policy2<G, XL::PROW>(W.xw, pol);
+        wave_lds_sync();
+        child_rows(k + 1, r1, v1);
+      } else {
+        float rsum, vsum;
+        expand_wave<G, XL::PROW, true>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+        wave_lds_sync();
+        child_rows(k, rsum, vsum);
+      }
+      if (st) st->wave_add(68, two ? 2 : 1);
+      wave_lds_sync();                       // W.ew / W.xw reused by the wave's next pair
+    }
+  } else if constexpr (XL::BATCH) {
     const int wave = __builtin_amdgcn_readfirstlane(wave_id());
     const int lane = lane_id_local();
     auto& W = L.wv[wave];

@@ -68,7 +68,9 @@ def main():
     sp = mzgo.SelfPlay(net, G, S, seed=1234)
     fn = _lib.lib.mzgo_debug_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    buf = np.zeros((G, 96), np.uint64)
+    # one row per tree slot (the move-parallel queue's workgroups at 19x19: one per CU)
+    rows = max(G, torch.cuda.get_device_properties(0).multi_processor_count)
+    buf = np.zeros((rows, 96), np.uint64)
     sp.reset(epoch=0)
     sp.move(sp.max_moves)                                     # warm-up epoch, stamps dropped
     torch.cuda.synchronize()
@@ -84,6 +86,25 @@ def main():
     c1 = sp.engine.counters()
     ms = a.elapsed_time(b)
     fn(sp.engine.handle, buf.ctypes.data_as(ctypes.c_void_p))
+    if os.environ.get("MZGO_MOVE_PARALLEL") == "1":
+        # the move-parallel epoch: the queue's workgroups have no games; phase
+        # shares over every slot row (the boards launch's own slots 83 / 87 too)
+        fa = buf.astype(np.float64)
+        # the boards launch runs no search: its per-move laps 84-86 and 88-90
+        # (representation, root, simulations) hold no interval there
+        fa[:, [84, 85, 86, 88, 89, 90]] = 0.0
+        tot = {k: float(fa[:, v].sum()) for k, v in PHASES.items()}
+        alls = sum(tot.values())
+        out = {"tag": tag, "workload": f"{N}x{N} Go self-play, {G} parallel games/GPU, {S} sims/move",
+               "schedule": "move-parallel (boards launch + k_search_queue)", "epoch_ms_stamps_build": ms,
+               "shares": {k: v / alls for k, v in tot.items()},
+               "cycles_per_workgroup": {k: v / rows for k, v in tot.items()},
+               "slots_sum": {int(i): float(fa[:, i].sum()) for i in range(fa.shape[1]) if fa[:, i].any()}}
+        d = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        json.dump(out, open(os.path.join(d, f"{tag}_phases.json"), "w"), indent=1)
+        print(json.dumps(out))
+        return
     f = buf[:G].astype(np.float64)
     game = f[:, MOVE_SLOTS].sum(1)                            # each game's busy cycles (its whole epoch)
     sims_slots = sorted({s for k, v in PHASES.items() if k not in ("representation", "board") for s in v} - {85})
