@@ -772,11 +772,9 @@ static bool move_parallel(const mzgo_engine* e, const SearchParams& sp, const Pl
   return pp.moves > 1 && !pp.arena && sp.compat == 0 && sp.variant == 0;
 }
 
-static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayParams& pp_in, hipStream_t s) {
+static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayParams& pp, hipStream_t s) {
   SearchParams sp = e->search_params();
-  PlayParams pp = pp_in;
   if (move_parallel(e, sp, pp)) {
-    pp.boards_only = 1;
     hipEvent_t* ev = nullptr;
     if (e->timing) {
       while ((int)e->tev.size() < 3 * (e->tn + 1)) {
@@ -788,7 +786,7 @@ static int launch_selfplay(mzgo_engine* e, const NetParams& np_b, const PlayPara
     }
     HIPCHK(hipMemsetAsync(e->E.mpq + 2 * e->G, 0, sizeof(int), s));
     if (ev) HIPCHK(hipEventRecord(ev[0], s));
-    HIPCHK(e->ks->selfplay_move(e->np, np_b, sp, pp, e->E, e->G, s));
+    HIPCHK(e->ks->selfplay_boards(sp, pp, e->E, e->G, s));
     if (ev) HIPCHK(hipEventRecord(ev[1], s));
     const int ncu = device_cus();
     int wg = ncu > 0 && ncu < e->TS ? ncu : e->TS;           // one tree slot per workgroup

@@ -25,6 +25,7 @@ struct KernelSet {
   hipError_t (*board_planes)(const EngineArrays&, int G, double* planes, hipStream_t);
   hipError_t (*selfplay_move)(const NetParams& np, const NetParams& np_b, const SearchParams&,
                               const PlayParams&, const EngineArrays&, int G, hipStream_t);
+  hipError_t (*selfplay_boards)(const SearchParams&, const PlayParams&, const EngineArrays&, int G, hipStream_t);
   hipError_t (*search_queue)(const NetParams& np, const SearchParams&, const PlayParams&, const EngineArrays&,
                              int G, int workgroups, hipStream_t);
 };
@@ -71,6 +72,10 @@ struct Launch {
                        pp, E);
     return hipGetLastError();
   }
+  static hipError_t boards(const SearchParams& sp, const PlayParams& pp, const EngineArrays& E, int G, hipStream_t s) {
+    hipLaunchKernelGGL((k_selfplay_boards<N, C>), dim3(G), dim3(BoardsGeo<Geo<N, C>>::THREADS), 0, s, sp, pp, E);
+    return hipGetLastError();
+  }
   static hipError_t queue(const NetParams& np, const SearchParams& sp, const PlayParams& pp, const EngineArrays& E,
                           int G, int workgroups, hipStream_t s) {
     hipLaunchKernelGGL((k_search_queue<N, C>), dim3(workgroups), dim3(Geo<N, C>::THREADS), 0, s, np, sp, pp, E, G);
@@ -81,7 +86,7 @@ struct Launch {
     return KernelSet{N, C, sizeof(Smem<G>), rep_needs_scratch<G>() ? 64 * N * N : 0,
                      Smem<G>::GLOBAL_Y ? 1 : 0, TailConvs<G>::value ? 1 : 0, &ii, &ri, &search, &breset, &bstep,
                      &bplanes,
-                     &move, &queue};
+                     &move, &boards, &queue};
   }
 };
 

@@ -2514,9 +2514,6 @@ struct PlayParams {
   int arena;              // 0: one network; 1: main.py's evaluator -- game i's first
                           // mover is network (i % 2), then the networks alternate
   int moves;              // moves per game in this launch (each game stops at its end)
-  int boards_only = 0;    // 1: the move-parallel epoch's first launch -- record, choose (compat
-                          // "reference": the action never reads the search) and step every
-                          // move, no search; k_search_queue then runs the searches
 };
 
 template <int N, int C>
@@ -2576,15 +2573,12 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #endif
       }
   };
-  if (pp.boards_only && tid_local() == 0) E_arg.mpq[2 * g + 1] = 0;
   if (E.status[g] != 0) { release_helpers(); tail_phase(); return; }
   if ((sp.helpers > 0 || sp.tail) && tid_local() == 0)
     __hip_atomic_store(job_of<G>(E_arg, g).started(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (G::WINO) wino_raw_zero<G>(sm.raw);        // zero halo of the conv input planes
   BoardMeta m;
   load_board<G>(sm, E, g, m);
-  const int mv_first = m.moves;
-  int played = 0;                                // moves recorded by this launch
   // pp.moves moves of this game in one launch (the board stays in LDS between
   // them): a game's moves run back to back on its CU instead of every move of
   // every game waiting for the slowest game's move at a launch boundary
@@ -2611,7 +2605,6 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     E.rec_invd[rec * G::CELLS + c] = sm.invd[c];
   }
   if (tid_local() == 0) E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
-  ++played;
 
   const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
   const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
@@ -2623,11 +2616,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 #endif
   SearchParams spm = launder_search(sp);
   spm.net = (pp.arena && (((pp.game_base + g) + mv) & 1)) ? 1 : 0;
-  if (pp.boards_only)
-    build_mask<G>(sm.t, sp.pass_epsilon, [&](int a) { return board_plane<G>(sm, m0, 3, a); });
-  else
-    run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
-                  tm ? tm + 2 : nullptr, noise_out);
+  run_search<G>(sm, np, spm, E, g, [&](int c, int j) { return board_plane<G>(sm, m0, c, j); }, noise, key,
+                tm ? tm + 2 : nullptr, noise_out);
 #ifdef MZGO_STAMPS
   tm[4] = __builtin_amdgcn_s_memtime();
 #endif
@@ -2640,10 +2630,8 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
     if (lane_id_local() == 0) {
       sm.bc[0] = a;
       E.rec_action[rec] = a;
-      if (!pp.boards_only) {                       // (the move-parallel epoch: k_search_queue)
-        const int n = T.visits[0];
-        E.rec_value[rec] = n > 0 ? T.wsum[0] / (double)n : 0.0;
-      }
+      const int n = T.visits[0];
+      E.rec_value[rec] = n > 0 ? T.wsum[0] / (double)n : 0.0;
     }
   }
   __syncthreads();
@@ -2687,13 +2675,139 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
   if (over) break;
   __syncthreads();                               // this move's LDS reads before the next move's writes
   }
-  // the moves this launch recorded (an erroring move included: it was searched)
-  if (pp.boards_only && tid_local() == 0) {
-    E_arg.mpq[2 * g] = mv_first;
-    E_arg.mpq[2 * g + 1] = played;
-  }
   release_helpers();
   tail_phase();
+}
+
+// ---------------------------------------------------------------------------
+// The move-parallel epoch, first launch: k_selfplay_move's boards-only path
+// (record, legal mask, action, board step, result; no search) as a kernel of
+// its own.  A game's moves are a serial chain of board steps, each a few
+// label-propagation rounds with a barrier apiece, so the step's latency is
+// the launch's: a workgroup of BoardsGeo::THREADS (one cell per lane, 2 waves
+// at 9x9) with a few KB of LDS instead of k_selfplay_move's 12 waves and 159
+// KB.  Same operations as the boards-only path (build_mask, choose_action,
+// board_step, board_winning with this workgroup as the team), so the records
+// are the same.
+// ---------------------------------------------------------------------------
+template <class G>
+struct BoardsGeo {
+  static constexpr int THREADS = (G::CELLS + 63) / 64 * 64 < 512 ? (G::CELLS + 63) / 64 * 64 : 512;
+};
+template <class G>
+struct BoardsTeam {
+  static constexpr int SIZE = BoardsGeo<G>::THREADS;
+  __device__ static int id() { return tid_local(); }
+  __device__ static void sync() { __syncthreads(); }
+  __device__ static bool any(int v) { return __syncthreads_or(v) != 0; }
+  __device__ static bool leader() { return tid_local() == 0; }
+};
+template <class G>
+struct BoardsSmem {
+  TreeLds<G> t;                                          // choose_action's mask and scratch
+  int label[G::CELLS], libs[G::CELLS], gsize[G::CELLS];
+  int8_t stone[G::CELLS];
+  uint8_t invd[G::CELLS];
+  int killed[4];
+  int misc[8];
+  int bc[8];
+};
+
+template <int N, int C>
+__global__ void __launch_bounds__((BoardsGeo<Geo<N, C>>::THREADS)) k_selfplay_boards(SearchParams sp, PlayParams pp,
+                                                                                    EngineArrays E) {
+  typedef Geo<N, C> G;
+  typedef BoardsTeam<G> T;
+  constexpr int BT = BoardsGeo<G>::THREADS;
+  __shared__ BoardsSmem<G> sm;
+  const int g = blockIdx.x;
+  const int tid = tid_local();
+  if (tid == 0) {
+    atomicAdd(&E.counters[6], 1ull);
+    E.mpq[2 * g + 1] = 0;
+  }
+  if (E.status[g] != 0) return;
+  for (int c = tid; c < G::CELLS; c += BT) {
+    sm.stone[c] = E.stones[(size_t)g * G::CELLS + c];
+    sm.invd[c] = E.invd[(size_t)g * G::CELLS + c];
+  }
+  BoardMeta m;
+  {
+    const int* mm = E.meta + g * 4;
+    m.turn = mm[0]; m.passed = mm[1]; m.done = mm[2]; m.moves = mm[3];
+  }
+  __syncthreads();
+  BoardLds<G> b;
+  b.stone = sm.stone; b.invd = sm.invd;
+  b.label = sm.label; b.libs = sm.libs; b.gsize = sm.gsize;
+  b.killed = sm.killed; b.misc = sm.misc;
+  const int mv_first = m.moves;
+  int played = 0;
+  const TreeView TV = TreeViewOf<G>::make(E, g);         // (compat "reference" reads no tree)
+  for (int step = 0; step < pp.moves; ++step) {
+    const int mv = m.moves;
+    const size_t rec = (size_t)g * E.max_moves + mv;
+    for (int c = tid; c < G::CELLS; c += BT) {
+      E.rec_stones[rec * G::CELLS + c] = sm.stone[c];
+      E.rec_invd[rec * G::CELLS + c] = sm.invd[c];
+    }
+    if (tid == 0) E.rec_flags[rec] = (uint8_t)(m.turn | (m.passed << 1) | (m.done << 2));
+    ++played;
+    const uint32_t gid = (uint32_t)(pp.game_base + g) ^ ((uint32_t)pp.epoch << 24);
+    const uint64_t key = stream_key(sp.seed, gid, (uint32_t)mv);
+    // build_mask (self_play.py:152, :363) with this workgroup's stride
+    {
+      int any = 0;
+      for (int a = tid; a < G::A; a += BT) {
+        const uint8_t v = a < G::CELLS ? (sm.invd[a] == 0 ? 1 : 0) : 1;
+        sm.t.valid[a] = v;
+        any |= (a < G::CELLS) && v;
+      }
+      any = __syncthreads_or(any);
+      if (tid == 0) sm.t.pass_prior = any ? sp.pass_epsilon : 1.0;
+      __syncthreads();
+    }
+    if (wave_id() == 0) {
+      const double temp = mv < pp.temperature_moves ? pp.temperature : 0.0;
+      const int a = choose_action<G>(sm.t, TV, sp.compat, temp, key, E.rec_policy + rec * G::A);
+      if (lane_id_local() == 0) {
+        sm.bc[0] = a;
+        E.rec_action[rec] = a;
+      }
+    }
+    __syncthreads();
+    const int action = sm.bc[0];
+    const int st = board_step<G, T>(b, m, action);
+    __syncthreads();
+    double w = 0.0;
+    if (st == BOARD_OK && m.done) w = board_winning<G, T>(b, pp.komi);
+    for (int c = tid; c < G::CELLS; c += BT) {
+      E.stones[(size_t)g * G::CELLS + c] = sm.stone[c];
+      E.invd[(size_t)g * G::CELLS + c] = sm.invd[c];
+    }
+    const bool over = st != BOARD_OK || m.done || m.moves >= E.max_moves;
+    if (tid == 0) {
+      int* mm = E.meta + g * 4;
+      mm[0] = m.turn; mm[1] = m.passed; mm[2] = m.done; mm[3] = m.moves;
+      E.rec_reward[rec] = w;
+      atomicAdd(&E.counters[0], (unsigned long long)sp.num_simulations);
+      atomicAdd(&E.counters[1], 1ull);
+      if (st != BOARD_OK) {
+        E.status[g] = 16 + st;
+      } else if (m.done || m.moves >= E.max_moves) {
+        E.status[g] = 1;
+        E.game_len[g] = m.moves;
+        E.final_reward[g] = m.done ? w : 0.0;
+        atomicAdd(&E.counters[2], 1ull);
+      }
+    }
+    if (over) break;
+    __syncthreads();                               // this move's LDS reads before the next move's writes
+  }
+  if (tid == 0) {
+    E.mpq[2 * g] = mv_first;
+    E.mpq[2 * g + 1] = played;
+  }
 }
 
 // ---------------------------------------------------------------------------
