@@ -44,3 +44,32 @@ def test_tower_roofline_arithmetic(batched, monkeypatch):
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     assert abs(r["towers_per_simulation"] - 110000 / 102400) < 1e-12
     assert r["kernel"] == ("k_tconv_chain<19>" if batched == "0" else "k_tconv_ks<19>")
+
+
+def test_selfplay_roofline_names_the_timed_kernel(tmp_path, monkeypatch):
+    """The move-parallel epoch's roofline is k_search_queue's: its avg launch
+    time is the one passed in, MFMA work per launch is the convs + the
+    representation per move, and a PMC profile is attached only when it is
+    of the same kernel (summarize_pmc stores the full demangled name)."""
+    import json
+    N, C, S, G = 9, 96, 200, 256
+    counts = dict(launches=2, sims=2 * 4.0e6, moves=2 * 20000.0, convs=2 * 150000.0, rows=2 * 140000.0)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    wl = "9x9 Go self-play, 256 parallel games/GPU, 200 sims/move"
+    pmc = {"tag": "t", "workload": wl, "dynamics": "factored", "moves_per_launch": 0, "n_gpus": 1,
+           "kernel": "void mzgo::k_search_queue<9, 96>(mzgo::NetParams, ...)", "avg_duration_ms": 30.0,
+           "counters": {"GRBM_GUI_ACTIVE": 8 * 2.4e9 * 0.030, "SQ_INSTS_VALU": 1.0e9, "SQ_LDS_IDX_ACTIVE": 4.0e9},
+           "hbm_bytes_per_launch": 1.5e10}
+    (prof / "latest_pmc.json").write_text(json.dumps(pmc))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    r = bench.roofline(N, C, S, G, counts, 0.030, "factored", wl, 0, 1, "k_search_queue")
+    assert r["kernel"] == "k_search_queue" and r["traffic"] == 1.5e10
+    assert abs(r["avg_launch_ms"] - 30.0) < 1e-9
+    per = 2048 * (150000 * bench.mfma_per_conv(N, C, C) + 20000 * (
+        9 * 2 * 4 * 6 + bench.mfma_per_conv(N, 64, 64) + bench.mfma_per_conv(N, 64, C)))
+    assert abs(r["units"]["mfma"]["per_launch"] - per) < 1e-6 * per
+    assert r["units"]["pmc_source"] == "profiles/t_pmc.json"
+    # a profile of the game-per-workgroup kernel is not this kernel's
+    r2 = bench.roofline(N, C, S, G, counts, 0.030, "factored", wl, 0, 1, "k_selfplay_move")
+    assert r2["traffic"] is None and "pmc_source" not in r2["units"]
