@@ -6,8 +6,8 @@ deterministic random-init weights, fp32.  One *step* = one whole self-play
 epoch: all 256 games from the empty board until
 every one has ended.  Under compat "reference" (the bench's protocol, SURVEY
 §0.6: the action is a uniform draw over the legal moves, never read from the
-search) an epoch is the move-parallel pair: k_selfplay_move with the searches
-left out records and steps every game's boards, then k_search_queue runs
+search) an epoch is the move-parallel pair: k_selfplay_boards records and
+steps every game's boards without their searches, then k_search_queue runs
 every recorded move's search (representation + root priors, 200 simulations
 of select / dynamics + prediction / expand / backup, the root value) from one
 queue on one workgroup per CU.  MZGO_MOVE_PARALLEL=0 times the

@@ -188,15 +188,18 @@ int mzgo_arena_moves(mzgo_engine* eng, mzgo_engine* opponent, int moves, void* s
 int mzgo_selfplay_counters(mzgo_engine* eng, uint64_t* counters_host, void* stream);
 
 /* Move-parallel epoch (no reference counterpart; the schedule, not the
- * protocol): a multi-move mzgo_selfplay_moves under compat "reference" on
- * 5x5-9x9 boards runs as two launches -- k_selfplay_move with the searches
- * left out (observation, action, policy target, board step and reward of
- * every move: under compat "reference" the action never reads the search)
- * and k_search_queue, which runs every recorded move's search (root value)
- * from one work queue on one workgroup per CU.  The records are byte-identical
- * to the game-per-workgroup launch (MZGO_MOVE_PARALLEL=0 in the environment
- * keeps that launch); the trees left in the slots are then those of whatever
- * searches ran last in each queue slot, not one per game.
+ * protocol): a multi-move mzgo_selfplay_moves under compat "reference"
+ * (self_play.py's search) runs as two launches -- k_selfplay_boards, every
+ * game's moves without their searches (observation, legal mask, action,
+ * policy target, board step, reward: under compat "reference" the action
+ * never reads the search), then k_search_queue, which runs every recorded
+ * move's search (root value) from one work queue on one workgroup per CU.
+ * The records are byte-identical to the game-per-workgroup launch
+ * (MZGO_MOVE_PARALLEL=0 in the environment keeps that launch); the trees
+ * left in the slots are then those of whatever searches ran last in each
+ * queue slot, not one per game.  19x19 engines created under compat
+ * "reference" hold a tree slot per CU for it (MZGO_MOVE_PARALLEL=0 at
+ * creation: G slots).
  * mzgo_selfplay_set_timing(eng, 1) records HIP events around both launches
  * of every such call (0 stops and discards); mzgo_selfplay_launch_times
  * synchronises on them, writes up to ``cap`` (boards, queue) durations in

@@ -112,7 +112,7 @@ struct EngineArrays {
   int* status;           // [G]  0 playing, 1 finished, >=16 error
   unsigned char* jobs;   // [G][job_bytes(A)] batch-expansion jobs shared with helper workgroups
   int* mpq;              // [2G + 1] move-parallel epoch (k_search_queue): per game (first move,
-                         // moves played) of the boards-only launch, then the queue head
+                         // moves played) of k_selfplay_boards, then the queue head
   unsigned long long* counters;  // [kCounters] 0: simulations run, 1: moves played, 2: games finished,
                                  //     3: dynamics convs run (factored: one per new parent; tower
                                  //     engines: towers evaluated, speculative ones included),
@@ -2680,13 +2680,13 @@ __global__ void __launch_bounds__((Geo<N, C>::THREADS)) __attribute__((amdgpu_wa
 }
 
 // ---------------------------------------------------------------------------
-// The move-parallel epoch, first launch: k_selfplay_move's boards-only path
-// (record, legal mask, action, board step, result; no search) as a kernel of
-// its own.  A game's moves are a serial chain of board steps, each a few
-// label-propagation rounds with a barrier apiece, so the step's latency is
+// The move-parallel epoch, first launch: every game's moves without their
+// searches (record, legal mask, action, board step, result).  A game's
+// moves are a serial chain of board steps, each a few label-propagation
+// rounds with a barrier apiece, so the step's latency is
 // the launch's: a workgroup of BoardsGeo::THREADS (one cell per lane, 2 waves
 // at 9x9) with a few KB of LDS instead of k_selfplay_move's 12 waves and 159
-// KB.  Same operations as the boards-only path (build_mask, choose_action,
+// KB.  Same operations as k_selfplay_move's move (build_mask, choose_action,
 // board_step, board_winning with this workgroup as the team), so the records
 // are the same.
 // ---------------------------------------------------------------------------

@@ -349,7 +349,7 @@ MP_CASES = [
 @pytest.mark.parametrize("N,G,S,per,epoch,qh", MP_CASES, ids=["9x9_g256_s200", "9x9_gcu44_s8_chunk16", "5x5_g64_s50",
                                                             "19x19_g16_s96", "19x19_g16_s96_qh1"])
 def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, qh, monkeypatch):
-    """The move-parallel epoch (compat "reference"; k_selfplay_move boards-only,
+    """The move-parallel epoch (compat "reference"; k_selfplay_boards,
     then k_search_queue: every recorded move's search claimed from one queue by
     a grid of one workgroup per CU, each in its own tree slot) against the
     game-per-workgroup launch (MZGO_MOVE_PARALLEL=0): byte-identical records
