@@ -416,6 +416,7 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
                                              Stamp* st = nullptr) {
   auto& L = sm.u.f;
   typedef decltype(sm.u.f) XL;
+  if (st && tid_local() == 0) { st->wave_add(48, 1); st->wave_add(55, (unsigned long long)B); }   // batches, children
   if constexpr (XL::GLOBAL_Y && !LAZY) {
     // Y streamed from L2 (19x19): a wave claims two children at a time and
     // reads the parent's Y once for both (expand_wave2)

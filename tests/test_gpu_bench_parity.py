@@ -340,6 +340,7 @@ MP_CASES = [
     (9, 256, 200, 0, 4, "0"),       # the headline's own launch
     (9, None, 8, 16, 2, "0"),       # more games than CUs (the queue's grid is the CU count), chunked launches
     (5, 64, 50, 0, 1, "0"),
+    (5, 64, 50, 7, 3, "inject"),    # injected Dirichlet samples (the oracle tests' hook), chunked launches
     (19, 16, 96, 0, 1, "0"),        # 19x19: a tree slot per CU (k_search_queue) vs 3 helper workgroups per game
     (19, 16, 96, 0, 2, "1"),        # 19x19: every searching workgroup with a helper (jobs per tree slot)
 ]
@@ -347,7 +348,8 @@ MP_CASES = [
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("N,G,S,per,epoch,qh", MP_CASES, ids=["9x9_g256_s200", "9x9_gcu44_s8_chunk16", "5x5_g64_s50",
-                                                            "19x19_g16_s96", "19x19_g16_s96_qh1"])
+                                                            "5x5_g64_s50_injected", "19x19_g16_s96",
+                                                            "19x19_g16_s96_qh1"])
 def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, qh, monkeypatch):
     """The move-parallel epoch (compat "reference"; k_selfplay_boards,
     then k_search_queue: every recorded move's search claimed from one queue by
@@ -364,7 +366,10 @@ def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, qh, 
     eng = sp.engine
     M = sp.max_moves
     out = {}
-    monkeypatch.setenv("MZGO_QUEUE_HELPERS", qh)
+    inject = qh == "inject"
+    monkeypatch.setenv("MZGO_QUEUE_HELPERS", "0" if inject else qh)
+    if inject:
+        eng.inject_noise(np.random.default_rng(7).dirichlet(np.full(eng.A, 0.3), size=(G, M)))
     for mode in ("1", "0"):
         monkeypatch.setenv("MZGO_MOVE_PARALLEL", mode)
         monkeypatch.setenv("MZGO_TAIL_HELPERS", "0")
@@ -380,6 +385,8 @@ def test_move_parallel_epoch_equals_game_per_workgroup(N, G, S, per, epoch, qh, 
         recs, arrays = _records(eng)
         out[mode] = (arrays, drawn.cpu().numpy(),
                      {k: c1[k] - c0[k] for k in c1 if k not in ("playing", "tail_wait_expiries")})
+    if inject:
+        eng.inject_noise(None)
     (aa, da, ca), (ab, db, cb) = out["1"], out["0"]
     if N == 19:
         # prior_rows counts the rows a game's own workgroup forms; with helper
