@@ -356,6 +356,8 @@ struct mzgo_engine {
     sp.helpers = 0;
     sp.net = 0;
     sp.tail = 0;
+    const char* lz = getenv("MZGO_LAZY_ROWS");        // (=0: eager rows in self-play too, an A/B switch)
+    sp.lazy_rows = lz && atoi(lz) == 0 ? 0 : 1;
     return sp;
   }
 };
@@ -670,8 +672,10 @@ int mzgo_search(mzgo_engine* e, const float* root_obs, const double* noise, int 
     HIPCHK(t.ts->search_out(t.TA, sp, e->E, G, visits, value, s));
     return check_chain(e, s);
   }
-  HIPCHK(e->ks->search(e->np, e->search_params(), e->E, root_obs, noise, G, e->cfg.game_base, move_index,
-                       visits, value, (hipStream_t)stream));
+  SearchParams sp = e->search_params();
+  sp.lazy_rows = 0;                                   // every row of an exported tree formed
+  HIPCHK(e->ks->search(e->np, sp, e->E, root_obs, noise, G, e->cfg.game_base, move_index, visits, value,
+                       (hipStream_t)stream));
   return MZGO_OK;
 }
 

@@ -352,7 +352,7 @@ struct Pol2 {
   static constexpr int SLOTS = (ExpandPlan<G>::PASSES + 7) / 8;
   float v[SLOTS];
 };
-template <class G, int PROW>
+template <class G, int PROW, bool POL = true>
 __device__ __forceinline__ void expand_wave2(float* xw, const float* yc, const float* ew0, const float* ew1,
                                              const float* hw, const ExpandPlan<G>& plan, float& rsum0,
                                              float& vsum0, float& rsum1, float& vsum1, Pol2<G>& pol1) {
@@ -366,11 +366,13 @@ __device__ __forceinline__ void expand_wave2(float* xw, const float* yc, const f
   f32x2 sa[X::PERL][2], sb[X::PERL][2];
 #pragma unroll
   for (int k = 0; k < X::PERL; ++k) {
-    wp[k] = W4[2 * X::C4 + j + 8 * k];
+    if constexpr (POL) wp[k] = W4[2 * X::C4 + j + 8 * k];
     sa[k][0] = sa[k][1] = sb[k][0] = sb[k][1] = f32x2{0.f, 0.f};
   }
+  if constexpr (POL) {
 #pragma unroll
-  for (int i = 0; i < Pol2<G>::SLOTS; ++i) pol1.v[i] = 0.f;
+    for (int i = 0; i < Pol2<G>::SLOTS; ++i) pol1.v[i] = 0.f;
+  }
   const f32x4* Y4 = reinterpret_cast<const f32x4*>(yc) + cg * X::C4 + j;
   const char* Eb0 = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew0) + j);
   const char* Eb1 = reinterpret_cast<const char*>(reinterpret_cast<const f32x4*>(ew1) + j);
@@ -388,25 +390,26 @@ __device__ __forceinline__ void expand_wave2(float* xw, const float* yc, const f
 #pragma unroll
       for (int q = 0; q < 4; q += 2) {
         const f32x2 yy = f32x2{y[k][q], y[k][q + 1]};
-        const f32x2 w2 = f32x2{wp[k][q], wp[k][q + 1]};
         f32x2 va = yy + f32x2{e0[k][q], e0[k][q + 1]};
         va.x = va.x > 0.f ? va.x : 0.f;
         va.y = va.y > 0.f ? va.y : 0.f;
-        ha = __builtin_elementwise_fma(w2, va, ha);
+        if constexpr (POL) ha = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, va, ha);
         if (!live) va = f32x2{0.f, 0.f};
         sa[k][q >> 1] = sa[k][q >> 1] + va;
         f32x2 vb = yy + f32x2{e1[k][q], e1[k][q + 1]};
         vb.x = vb.x > 0.f ? vb.x : 0.f;
         vb.y = vb.y > 0.f ? vb.y : 0.f;
-        hb = __builtin_elementwise_fma(w2, vb, hb);
+        if constexpr (POL) hb = __builtin_elementwise_fma(f32x2{wp[k][q], wp[k][q + 1]}, vb, hb);
         if (!live) vb = f32x2{0.f, 0.f};
         sb[k][q >> 1] = sb[k][q >> 1] + vb;
       }
     }
-    xr[8 * p] = sum8(ha.x + ha.y);
-    const float pb = sum8(hb.x + hb.y);
+    if constexpr (POL) {
+      xr[8 * p] = sum8(ha.x + ha.y);
+      const float pb = sum8(hb.x + hb.y);
 #pragma unroll
-    for (int i = 0; i < Pol2<G>::SLOTS; ++i) pol1.v[i] = p == 8 * i + j ? pb : pol1.v[i];
+      for (int i = 0; i < Pol2<G>::SLOTS; ++i) pol1.v[i] = p == 8 * i + j ? pb : pol1.v[i];
+    }
   };
   f32x4 ya[X::PERL], yb[X::PERL];
   auto ldy = [&](int p, f32x4 (&y)[X::PERL]) {

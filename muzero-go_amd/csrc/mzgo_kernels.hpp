@@ -441,6 +441,18 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
       child_priors<G>(sm.t, x, TV.prior + (size_t)nid * G::A, -1, sp.variant, W.fscratch(), W.dscratch());
       if (lane == 0) L.bv[k] = (double)r + sp.discount * (double)v;
     };
+    // the lazy policy head (sp.lazy_rows; self-play): the totals only, and
+    // the sentinel kLazyRow in child-row entry 0 -- a select that first
+    // reaches the node forms its logits and priors (expand_child's LAZYH)
+    auto lazy_child = [&](int k, float rsum, float vsum) {
+      float r, v;
+      heads_from_totals<G>(rsum, vsum, sm.t.hsc, r, v);
+      if (lane == 0) {
+        TV.child[(size_t)(nid0 + k) * G::A] = kLazyRow;
+        L.bv[k] = (double)r + sp.discount * (double)v;
+      }
+    };
+    const bool lazy = sp.lazy_rows != 0;
     for (;;) {
       int k = 0;
       if (lane == 0) k = atomicAdd(&sm.t.ngrab, 2);
@@ -459,7 +471,19 @@ __device__ __forceinline__ void batch_expand(Smem<G>& sm, const NetParams& np, c
         for (int i = lane; i < E4N; i += 64) ew1[i] = e1[i];
       }
       wave_lds_sync();
-      if (two) {
+      if (lazy) {
+        if (two) {
+          float r0, v0, r1, v1;
+          Pol2<G> pol;
+          expand_wave2<G, XL::PROW, false>(W.xw, yg, W.ew, W.ew2, L.hw, plan, r0, v0, r1, v1, pol);
+          lazy_child(k, r0, v0);
+          lazy_child(k + 1, r1, v1);
+        } else {
+          float rsum, vsum;
+          expand_wave<G, XL::PROW, false>(W.xw, yg, W.ew, L.hw, plan, rsum, vsum);
+          lazy_child(k, rsum, vsum);
+        }
+      } else if (two) {
         float r0, v0, r1, v1;
         Pol2<G> pol;
         expand_wave2<G, XL::PROW>(W.xw, yg, W.ew, W.ew2, L.hw, plan, r0, v0, r1, v1, pol);
@@ -1842,11 +1866,14 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
   // prior rows formed (HBM writes of a node's priors + child row): eager
   // expansions, and lazily expanded nodes on a select's first arrival
   int rows = 0;
+  // (batched children with eager rows: the HBM trees' non-shared batches
+  // unless self-play keeps their policy head lazy, sp.lazy_rows)
+  const bool eager_rows = !(Acc::LDS || shared_jobs<G>(sp) || (decltype(sm.u.f)::GLOBAL_Y && sp.lazy_rows));
   Stamp st(E.stamps);
   int sim = 0;
   if (factored) {
     sim = root_batch<G, Acc>(sm, np, sp, E, g, TV, T, pool, scratch, nact, key, &st);
-    if (!(Acc::LDS || shared_jobs<G>(sp))) rows += sim;
+    if (eager_rows) rows += sim;
     nodes += sim;
     convs += sim > 0 ? 1 : 0;
     st.lap(4);
@@ -2019,7 +2046,7 @@ __device__ __forceinline__ void sim_loop(Smem<G>& sm, const NetParams& np, const
         }
         __syncthreads();
         st.lap(5);
-        if (!(Acc::LDS || shared_jobs<G>(sp))) rows += B;
+        if (eager_rows) rows += B;
         if (replay_parallel(shared_jobs<G>(sp), B, depth)) {
           const int m = verify_batch<G, Acc>(sm, sp, E, g, TV, T, nact, leaf, depth, B, nid, &st, shared_jobs<G>(sp));
           nodes += m;

@@ -32,6 +32,9 @@ struct SearchParams {
   int net;                  // k_selfplay_move: the network of this move (arena: 1 = np_b), for the helpers
   int tail;                 // 9x9 whole-game launches: a workgroup whose game has ended helps running
                             // games with their parent convs (tail_help; 0: off)
+  int lazy_rows;            // Y-streaming boards (19x19) without helpers: batched children keep the
+                            // lazy policy head (kLazyRow, as the shared batches do); 0: eager rows
+                            // (mzgo_search, whose trees are exported whole)
 };
 
 // One game's tree (global memory).  Node 0 is the root; node ids grow by one
